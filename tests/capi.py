@@ -1,0 +1,208 @@
+"""ctypes driver for the zfp C API (include/zfp.h).
+
+The same calls drive either the reference build (oracle/_ref/libzfp_ref.so) or
+this framework's product library (zfp-par_amd/lib/libzfp.so), which exports the
+identical symbols -- so parity tests read like the reference's own end-to-end
+tests (tests/src/endtoend/zfpEndtoendBase.c): build a field, set a mode, open a
+bitstream on a buffer, zfp_compress / zfp_decompress, compare bytes.
+"""
+import ctypes
+
+import numpy as np
+
+ZFP_HEADER_FULL = 7
+TYPE_OF = {np.dtype(np.int32): 1, np.dtype(np.int64): 2, np.dtype(np.float32): 3, np.dtype(np.float64): 4}
+DTYPE_OF = {1: np.int32, 2: np.int64, 3: np.float32, 4: np.float64}
+
+vp = ctypes.c_void_p
+sz = ctypes.c_size_t
+u32 = ctypes.c_uint
+i32 = ctypes.c_int
+dbl = ctypes.c_double
+u64 = ctypes.c_uint64
+pd = ctypes.c_ssize_t
+
+
+class ZfpField(ctypes.Structure):
+    """zfp_field layout: zfp.h:135-140."""
+    _fields_ = [("type", i32), ("nx", sz), ("ny", sz), ("nz", sz), ("nw", sz),
+                ("sx", pd), ("sy", pd), ("sz", pd), ("sw", pd), ("data", vp)]
+
+
+class ZfpCAPI:
+    _SIGS = {
+        "zfp_stream_open": (vp, [vp]),
+        "zfp_stream_close": (None, [vp]),
+        "zfp_stream_set_bit_stream": (None, [vp, vp]),
+        "zfp_stream_rewind": (None, [vp]),
+        "zfp_stream_set_rate": (dbl, [vp, dbl, i32, u32, i32]),
+        "zfp_stream_set_precision": (u32, [vp, u32]),
+        "zfp_stream_set_accuracy": (dbl, [vp, dbl]),
+        "zfp_stream_set_reversible": (None, [vp]),
+        "zfp_stream_set_params": (i32, [vp, u32, u32, u32, i32]),
+        "zfp_stream_set_mode": (i32, [vp, u64]),
+        "zfp_stream_mode": (u64, [vp]),
+        "zfp_stream_compression_mode": (i32, [vp]),
+        "zfp_stream_params": (None, [vp, vp, vp, vp, vp]),
+        "zfp_stream_rate": (dbl, [vp, u32]),
+        "zfp_stream_precision": (u32, [vp]),
+        "zfp_stream_accuracy": (dbl, [vp]),
+        "zfp_stream_maximum_size": (sz, [vp, vp]),
+        "zfp_stream_maximum_size_chunk": (sz, [vp, vp, vp]),
+        "zfp_stream_set_execution": (i32, [vp, i32]),
+        "zfp_stream_execution": (i32, [vp]),
+        "zfp_stream_compressed_size": (sz, [vp]),
+        "zfp_field_alloc": (vp, []),
+        "zfp_field_1d": (vp, [vp, i32, sz]),
+        "zfp_field_2d": (vp, [vp, i32, sz, sz]),
+        "zfp_field_3d": (vp, [vp, i32, sz, sz, sz]),
+        "zfp_field_4d": (vp, [vp, i32, sz, sz, sz, sz]),
+        "zfp_field_free": (None, [vp]),
+        "zfp_field_set_pointer": (None, [vp, vp]),
+        "zfp_field_set_stride_3d": (None, [vp, pd, pd, pd]),
+        "zfp_field_set_stride_4d": (None, [vp, pd, pd, pd, pd]),
+        "zfp_field_metadata": (u64, [vp]),
+        "zfp_field_set_metadata": (i32, [vp, u64]),
+        "zfp_field_blocks": (sz, [vp]),
+        "zfp_field_size": (sz, [vp, vp]),
+        "zfp_compress": (sz, [vp, vp]),
+        "zfp_decompress": (sz, [vp, vp]),
+        "zfp_compress_chunk": (sz, [vp, vp, vp]),
+        "zfp_decompress_chunk": (sz, [vp, vp, vp]),
+        "zfp_write_header": (sz, [vp, vp, u32]),
+        "zfp_read_header": (sz, [vp, vp, u32]),
+        "zfp_chunk_alloc": (vp, []),
+        "zfp_chunk_free": (None, [vp]),
+        "zfp_set_chunk_3d": (None, [vp, i32, i32, i32, i32, i32, i32]),
+        "zfp_set_chunk_4d": (None, [vp, i32, i32, i32, i32, i32, i32, i32, i32]),
+        "zfp_optimal_parts_from_size": (vp, [i32, vp, ctypes.c_float, i32]),
+        "zfp_chunks_from_blocks": (vp, [i32, vp, vp]),
+        "zfp_blocks_free": (None, [vp]),
+        "zfp_chunks_free": (None, [vp]),
+        "zfp_break_axis": (i32, [i32, i32, vp, vp]),
+        "stream_open": (vp, [vp, sz]),
+        "stream_close": (None, [vp]),
+        "stream_size": (sz, [vp]),
+        "stream_wtell": (u64, [vp]),
+        "stream_rtell": (u64, [vp]),
+        "stream_write_bits": (u64, [vp, u64, u32]),
+        "stream_read_bits": (u64, [vp, u32]),
+        "stream_flush": (u64, [vp]),
+        "stream_align": (u64, [vp]),
+        "stream_rewind": (None, [vp]),
+        "stream_pad": (None, [vp, u64]),
+        "stream_skip": (None, [vp, u64]),
+        "stream_rseek": (None, [vp, u64]),
+        "stream_wseek": (None, [vp, u64]),
+    }
+
+    def __init__(self, path):
+        self.path = path
+        self.lib = ctypes.CDLL(path)
+        for name, (res, args) in self._SIGS.items():
+            fn = getattr(self.lib, name)
+            fn.restype = res
+            fn.argtypes = args
+
+    def __getattr__(self, name):
+        return getattr(self.lib, name)
+
+    # ---- helpers mirroring the reference's own call sequences ----
+    def field_for(self, arr, strided=False):
+        """numpy array -> zfp_field (x fastest = last numpy axis)."""
+        t = TYPE_OF[arr.dtype]
+        shp = list(reversed(arr.shape))
+        ptr = arr.ctypes.data
+        if arr.ndim == 1:
+            f = self.lib.zfp_field_1d(ptr, t, *shp)
+        elif arr.ndim == 2:
+            f = self.lib.zfp_field_2d(ptr, t, *shp)
+        elif arr.ndim == 3:
+            f = self.lib.zfp_field_3d(ptr, t, *shp)
+        else:
+            f = self.lib.zfp_field_4d(ptr, t, *shp)
+        if strided:
+            st = [s // arr.itemsize for s in reversed(arr.strides)]
+            if arr.ndim == 3:
+                self.lib.zfp_field_set_stride_3d(f, *st)
+            elif arr.ndim == 4:
+                self.lib.zfp_field_set_stride_4d(f, *st)
+        return f
+
+    def set_mode(self, zs, mode, param=None, ztype=0, dims=3):
+        if mode == "rate":
+            self.lib.zfp_stream_set_rate(zs, float(param), ztype, dims, 0)
+        elif mode == "precision":
+            self.lib.zfp_stream_set_precision(zs, int(param))
+        elif mode == "accuracy":
+            self.lib.zfp_stream_set_accuracy(zs, float(param))
+        elif mode == "reversible":
+            self.lib.zfp_stream_set_reversible(zs)
+        elif mode == "expert":
+            self.lib.zfp_stream_set_params(zs, *param)
+        else:
+            raise ValueError(mode)
+
+    def compress(self, arr, mode, param=None, ztype=None, header=False, chunk=None, strided=False,
+                 execution=None):
+        """Returns the compressed bytes exactly as zfp_compress leaves them."""
+        if ztype is None:
+            ztype = TYPE_OF[arr.dtype]
+        field = self.field_for(arr, strided)
+        zs = self.lib.zfp_stream_open(None)
+        self.set_mode(zs, mode, param, ztype, arr.ndim)
+        if execution is not None:
+            assert self.lib.zfp_stream_set_execution(zs, execution)
+        cap = self.lib.zfp_stream_maximum_size(zs, field) + 64
+        buf = np.zeros(cap, dtype=np.uint8)
+        bs = self.lib.stream_open(buf.ctypes.data, cap)
+        self.lib.zfp_stream_set_bit_stream(zs, bs)
+        self.lib.zfp_stream_rewind(zs)
+        if header:
+            assert self.lib.zfp_write_header(zs, field, ZFP_HEADER_FULL)
+        if chunk is None:
+            n = self.lib.zfp_compress(zs, field)
+        else:
+            ck = self.make_chunk(arr.ndim, chunk)
+            n = self.lib.zfp_compress_chunk(zs, ck, field)
+            self.lib.zfp_chunk_free(ck)
+        self.lib.stream_close(bs)
+        self.lib.zfp_stream_close(zs)
+        self.lib.zfp_field_free(field)
+        return bytes(buf[:n])
+
+    def decompress(self, data, shape, dtype, mode, param=None, ztype=None, header=False, out=None,
+                   execution=None):
+        dtype = np.dtype(dtype)
+        if out is None:
+            out = np.zeros(shape, dtype=dtype)
+        if ztype is None:
+            ztype = TYPE_OF[dtype]
+        field = self.field_for(out)
+        zs = self.lib.zfp_stream_open(None)
+        self.set_mode(zs, mode, param, ztype, len(shape))
+        if execution is not None:
+            assert self.lib.zfp_stream_set_execution(zs, execution)
+        buf = np.frombuffer(bytearray(data) + bytearray(64), dtype=np.uint8)
+        bs = self.lib.stream_open(buf.ctypes.data, len(data))
+        self.lib.zfp_stream_set_bit_stream(zs, bs)
+        self.lib.zfp_stream_rewind(zs)
+        if header:
+            assert self.lib.zfp_read_header(zs, field, ZFP_HEADER_FULL)
+        n = self.lib.zfp_decompress(zs, field)
+        self.lib.stream_close(bs)
+        self.lib.zfp_stream_close(zs)
+        self.lib.zfp_field_free(field)
+        return out, n
+
+    def make_chunk(self, ndim, box):
+        """box: list of (f, e) per zfp axis (x first)."""
+        ck = self.lib.zfp_chunk_alloc()
+        if ndim == 3:
+            self.lib.zfp_set_chunk_3d(ck, box[0][0], box[1][0], box[2][0], box[0][1], box[1][1], box[2][1])
+        elif ndim == 4:
+            self.lib.zfp_set_chunk_4d(ck, box[0][0], box[1][0], box[2][0], box[3][0],
+                                      box[0][1], box[1][1], box[2][1], box[3][1])
+        else:
+            raise ValueError("chunk helper covers 3D/4D")
+        return ck

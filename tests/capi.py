@@ -143,6 +143,24 @@ class ZfpCAPI:
         else:
             raise ValueError(mode)
 
+    def enable_index(self):
+        """Product library only: bind the MI355X block-index extension."""
+        for name, res, args in [("zfp_stream_hip_index", vp, [vp]), ("zfp_stream_set_hip_index", i32, [vp, vp]),
+                                ("zfp_hip_index_free", None, [vp]), ("zfp_hip_device_count", i32, []),
+                                ("zfp_hip_last_timing", i32, [vp, vp]), ("zfp_hip_last_error", ctypes.c_char_p, [])]:
+            fn = getattr(self.lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        self.keep_index = True
+        self.last_index = None
+
+    def _take_index(self, zs):
+        if getattr(self, "keep_index", False):
+            idx = self.lib.zfp_stream_hip_index(zs)
+            if idx:
+                self.lib.zfp_stream_set_hip_index(zs, idx)  # caller-owned from here on
+            self.last_index = idx
+
     def compress(self, arr, mode, param=None, ztype=None, header=False, chunk=None, strided=False,
                  execution=None):
         """Returns the compressed bytes exactly as zfp_compress leaves them."""
@@ -166,13 +184,14 @@ class ZfpCAPI:
             ck = self.make_chunk(arr.ndim, chunk)
             n = self.lib.zfp_compress_chunk(zs, ck, field)
             self.lib.zfp_chunk_free(ck)
+        self._take_index(zs)
         self.lib.stream_close(bs)
         self.lib.zfp_stream_close(zs)
         self.lib.zfp_field_free(field)
         return bytes(buf[:n])
 
     def decompress(self, data, shape, dtype, mode, param=None, ztype=None, header=False, out=None,
-                   execution=None):
+                   execution=None, index=None):
         dtype = np.dtype(dtype)
         if out is None:
             out = np.zeros(shape, dtype=dtype)
@@ -189,6 +208,8 @@ class ZfpCAPI:
         self.lib.zfp_stream_rewind(zs)
         if header:
             assert self.lib.zfp_read_header(zs, field, ZFP_HEADER_FULL)
+        if index is not None:
+            self.lib.zfp_stream_set_hip_index(zs, index)
         n = self.lib.zfp_decompress(zs, field)
         self.lib.stream_close(bs)
         self.lib.zfp_stream_close(zs)

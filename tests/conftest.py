@@ -39,6 +39,26 @@ def ref_capi():
     return ZfpCAPI(REF_SO)
 
 
+PRODUCT_SO = os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so")
+
+
+@pytest.fixture(scope="session")
+def product():
+    """The product library; GPU tests fail loudly if it or the GPU is missing."""
+    if not os.path.exists(PRODUCT_SO):
+        raise RuntimeError("zfp-par_amd/lib/libzfp.so is not built (python -c 'import __graft_entry__ as g; g.build()')")
+    try:  # one HIP runtime per process: let torch's (same SONAME) load first
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    from capi import ZfpCAPI
+    api = ZfpCAPI(PRODUCT_SO)
+    api.enable_index()
+    if api.lib.zfp_hip_device_count() <= 0:
+        raise RuntimeError("no HIP device visible: the MI355X path cannot run")
+    return api
+
+
 @pytest.fixture(scope="session")
 def golden():
     import json

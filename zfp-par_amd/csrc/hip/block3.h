@@ -1,0 +1,461 @@
+// Per-lane codec of one 4x4x4 block (float or double) for every zfp mode.
+//
+// encode_block3: lossy (encodef.c:63-90 + encode.c:260-280) and reversible
+//                (revencodef.c:45-80 + revencode.c:54-76) block encoders.
+// decode_block3: decodef.c:7-36 + decode.c:271-287, revdecodef.c:22-59 +
+//                revdecode.c:34-52.
+// Block gather/scatter with partial-block padding: encode3.c:5-31 /
+// decode3.c:5-23, pad rule encode.c:9-27.
+#pragma once
+
+#include "codec_dev.h"
+
+namespace zfp_amd {
+
+// pad a partial line of n valid values (n >= 1 here; n == 0 cannot occur
+// for a block whose origin lies inside the field)
+template <typename S>
+__device__ __forceinline__ void pad_line(S* v, int b, int s, int n)
+{
+  if (n <= 1) v[b + s] = v[b];
+  if (n <= 2) v[b + 2 * s] = v[b + s];
+  if (n <= 3) v[b + 3 * s] = v[b];
+}
+
+struct Geometry {
+  uint64_t n[4];
+  int64_t s[4];
+  uint64_t f[4];
+  uint32_t nb[4];  // blocks per axis in the chunk box
+  uint64_t nblocks;
+};
+
+struct BlockPos {
+  int64_t off;  // element offset of the block origin
+  int cnt[4];   // valid extent per axis (<= 4)
+  bool full;
+};
+
+__device__ __forceinline__ BlockPos block_pos(const Geometry& g, uint64_t b, int dims)
+{
+  BlockPos p;
+  p.off = 0;
+  p.full = true;
+#pragma unroll
+  for (int a = 0; a < 4; a++) {
+    p.cnt[a] = 4;
+    if (a < dims) {
+      uint64_t nb = g.nb[a];
+      uint64_t bi = (a == dims - 1) ? b : b % nb;
+      b = (a == dims - 1) ? 0 : b / nb;
+      uint64_t x = g.f[a] + 4 * bi;
+      uint64_t left = g.n[a] - x;
+      p.cnt[a] = left < 4 ? (int)left : 4;
+      p.full = p.full && left >= 4;
+      p.off += (int64_t)x * g.s[a];
+    }
+  }
+  return p;
+}
+
+template <typename S, bool VEC>
+__device__ __forceinline__ void gather3(S (&v)[64], const S* __restrict__ base, const Geometry& g, const BlockPos& p)
+{
+  const S* o = base + p.off;
+  const int64_t sx = g.s[0], sy = g.s[1], sz = g.s[2];
+  if (p.full) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        const S* r = o + j * sy + k * sz;
+        if (VEC) {
+          if constexpr (sizeof(S) == 4) {
+            float4 q = *reinterpret_cast<const float4*>(r);
+            v[16 * k + 4 * j + 0] = q.x;
+            v[16 * k + 4 * j + 1] = q.y;
+            v[16 * k + 4 * j + 2] = q.z;
+            v[16 * k + 4 * j + 3] = q.w;
+          } else {
+            double2 q0 = *reinterpret_cast<const double2*>(r);
+            double2 q1 = *reinterpret_cast<const double2*>(r + 2);
+            v[16 * k + 4 * j + 0] = q0.x;
+            v[16 * k + 4 * j + 1] = q0.y;
+            v[16 * k + 4 * j + 2] = q1.x;
+            v[16 * k + 4 * j + 3] = q1.y;
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            v[16 * k + 4 * j + i] = r[i * sx];
+        }
+      }
+  } else {
+    const int cx = p.cnt[0], cy = p.cnt[1], cz = p.cnt[2];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          v[16 * k + 4 * j + i] = (i < cx && j < cy && k < cz) ? o[i * sx + j * sy + k * sz] : (S)0;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        if (k < cz && j < cy) pad_line(v, 16 * k + 4 * j, 1, cx);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        if (k < cz) pad_line(v, 16 * k + i, 4, cy);
+#pragma unroll
+    for (int j = 0; j < 4; j++)
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        pad_line(v, 4 * j + i, 16, cz);
+  }
+}
+
+template <typename S, bool VEC>
+__device__ __forceinline__ void scatter3(const S (&v)[64], S* __restrict__ base, const Geometry& g, const BlockPos& p)
+{
+  S* o = base + p.off;
+  const int64_t sx = g.s[0], sy = g.s[1], sz = g.s[2];
+  if (p.full) {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        S* r = o + j * sy + k * sz;
+        if (VEC) {
+          if constexpr (sizeof(S) == 4) {
+            float4 q = make_float4(v[16 * k + 4 * j + 0], v[16 * k + 4 * j + 1], v[16 * k + 4 * j + 2],
+                                   v[16 * k + 4 * j + 3]);
+            *reinterpret_cast<float4*>(r) = q;
+          } else {
+            *reinterpret_cast<double2*>(r) = make_double2(v[16 * k + 4 * j + 0], v[16 * k + 4 * j + 1]);
+            *reinterpret_cast<double2*>(r + 2) = make_double2(v[16 * k + 4 * j + 2], v[16 * k + 4 * j + 3]);
+          }
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; i++)
+            r[i * sx] = v[16 * k + 4 * j + i];
+        }
+      }
+  } else {
+    const int cx = p.cnt[0], cy = p.cnt[1], cz = p.cnt[2];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          if (i < cx && j < cy && k < cz) o[i * sx + j * sy + k * sz] = v[16 * k + 4 * j + i];
+  }
+}
+
+// ---- coefficient order + negabinary, then bit planes ----
+__device__ __forceinline__ void planes_from_coeffs(uint64_t (&P)[32], const int32_t (&q)[64])
+{
+  uint32_t lo[32], hi[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    lo[i] = ((uint32_t)q[kPerm3[i]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    hi[i] = ((uint32_t)q[kPerm3[i + 32]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+  }
+  transpose32(lo);
+  transpose32(hi);
+#pragma unroll
+  for (int k = 0; k < 32; k++)
+    P[k] = (uint64_t)lo[k] | ((uint64_t)hi[k] << 32);
+}
+
+// double: planes 32..63 from the high words; 0..31 only when `need_low`
+__device__ __forceinline__ void planes_from_coeffs(uint64_t (&P)[64], const int64_t (&q)[64], bool need_low)
+{
+  uint32_t a[32], b[32];
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    uint64_t u0 = ((uint64_t)q[kPerm3[i]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    uint64_t u1 = ((uint64_t)q[kPerm3[i + 32]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    a[i] = (uint32_t)(u0 >> 32);
+    b[i] = (uint32_t)(u1 >> 32);
+  }
+  transpose32(a);
+  transpose32(b);
+#pragma unroll
+  for (int k = 0; k < 32; k++)
+    P[32 + k] = (uint64_t)a[k] | ((uint64_t)b[k] << 32);
+  if (__any(need_low)) {
+#pragma unroll
+    for (int i = 0; i < 32; i++) {
+      uint64_t u0 = ((uint64_t)q[kPerm3[i]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+      uint64_t u1 = ((uint64_t)q[kPerm3[i + 32]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+      a[i] = (uint32_t)u0;
+      b[i] = (uint32_t)u1;
+    }
+    transpose32(a);
+    transpose32(b);
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+      P[k] = (uint64_t)a[k] | ((uint64_t)b[k] << 32);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; k++)
+      P[k] = 0;
+  }
+}
+
+__device__ __forceinline__ void coeffs_from_planes(int32_t (&q)[64], const uint64_t (&P)[32])
+{
+  uint32_t lo[32], hi[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    lo[k] = (uint32_t)P[k];
+    hi[k] = (uint32_t)(P[k] >> 32);
+  }
+  transpose32(lo);
+  transpose32(hi);
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    q[kPerm3[i]] = (int32_t)((lo[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+    q[kPerm3[i + 32]] = (int32_t)((hi[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+  }
+}
+
+__device__ __forceinline__ void coeffs_from_planes(int64_t (&q)[64], const uint64_t (&P)[64], bool need_low)
+{
+  uint32_t a[32], b[32], c[32], d[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    a[k] = (uint32_t)P[32 + k];
+    b[k] = (uint32_t)(P[32 + k] >> 32);
+  }
+  transpose32(a);
+  transpose32(b);
+  if (__any(need_low)) {
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+      c[k] = (uint32_t)P[k];
+      d[k] = (uint32_t)(P[k] >> 32);
+    }
+    transpose32(c);
+    transpose32(d);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 32; k++) {
+      c[k] = 0;
+      d[k] = 0;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    uint64_t u0 = ((uint64_t)a[i] << 32) | c[i];
+    uint64_t u1 = ((uint64_t)b[i] << 32) | d[i];
+    q[kPerm3[i]] = (int64_t)((u0 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+    q[kPerm3[i + 32]] = (int64_t)((u1 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+  }
+}
+
+__device__ __forceinline__ uint32_t precision3(int emax, const CodecParams& cp)
+{
+  int p = emax - cp.minexp + 2 * 3 + 2;
+  if (p < 0) p = 0;
+  return (uint32_t)p < cp.maxprec ? (uint32_t)p : cp.maxprec;
+}
+
+// integer part of the block: order, planes, coder (encode.c:260-280)
+template <typename Int>
+__device__ __forceinline__ uint32_t encode_ints3(SlotWriter& w, Int (&q)[64], uint32_t budget, uint32_t prec)
+{
+  using S = typename std::conditional<sizeof(Int) == 4, float, double>::type;
+  constexpr int PREC = Traits<S>::kIntPrec;
+  uint64_t P[PREC];
+  if constexpr (PREC == 32)
+    planes_from_coeffs(P, q);
+  else
+    planes_from_coeffs(P, q, prec > 32);
+  return code_planes64<PREC>(w, budget, prec, P);
+}
+
+template <typename Int>
+__device__ __forceinline__ uint32_t decode_ints3(WordReader& r, Int (&q)[64], uint32_t budget, uint32_t prec)
+{
+  using S = typename std::conditional<sizeof(Int) == 4, float, double>::type;
+  constexpr int PREC = Traits<S>::kIntPrec;
+  uint64_t P[PREC];
+  uint32_t used = decode_planes64<PREC>(r, budget, prec, P);
+  if constexpr (PREC == 32)
+    coeffs_from_planes(q, P);
+  else
+    coeffs_from_planes(q, P, prec > 32);
+  return used;
+}
+
+// Encode one block; returns its length in bits including minbits padding
+// (padding bits are zeros and are NOT written to the slot).
+template <typename S, bool REV>
+__device__ __forceinline__ uint32_t encode_block3(SlotWriter& w, S (&v)[64], const CodecParams& cp)
+{
+  using T = Traits<S>;
+  using Int = typename T::Int;
+  using UInt = typename T::UInt;
+  constexpr uint32_t kE = T::kEbits;
+  Int q[64];
+  if constexpr (REV) {
+    // reversible (revencodef.c:45-80)
+    int emax = block_emax(block_absmax(v));
+    bool same = true;
+    if (emax != -T::kEbias) {
+      fwd_cast(q, v, emax);
+      S s = (sizeof(S) == 4) ? (S)pow2f(emax - 30) : (S)pow2d(emax - 62);
+#pragma unroll
+      for (int i = 0; i < 64; i++)
+        same = same && (bits_of((S)(s * (S)q[i])) == bits_of(v[i]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; i++) {
+        q[i] = 0;
+        same = same && (bits_of(v[i]) == 0);
+      }
+    }
+    uint32_t bits;
+    if (same) {
+      uint32_t e = (uint32_t)(emax + T::kEbias);
+      if (!e) {
+        w.put(0, 1);
+        return 1;
+      }
+      w.put(1, 2);
+      w.put(e, kE);
+      bits = 2 + kE;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; i++) {
+        Int x = (Int)bits_of(v[i]);
+        q[i] = x < 0 ? (Int)((UInt)x ^ T::kTcMask) : x;
+      }
+      w.put(3, 2);
+      bits = 2;
+    }
+    // rev_encode_block_<Int> (revencode.c:54-76)
+    uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
+    uint32_t maxb = cp.maxbits - bits;
+    xform<3, false, true>(q);
+    UInt all = 0;
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      all |= ((UInt)q[i] + T::kNbMask) ^ T::kNbMask;
+    uint32_t prec = all ? (uint32_t)(T::kIntPrec - (sizeof(S) == 4 ? __builtin_ctz((uint32_t)all)
+                                                                    : __builtin_ctzll((uint64_t)all)))
+                        : 0u;
+    if (prec > cp.maxprec) prec = cp.maxprec;
+    if (prec < 1) prec = 1;
+    w.put(prec - 1, T::kPbits);
+    uint32_t ib = T::kPbits + encode_ints3(w, q, maxb - T::kPbits, prec);
+    if (ib < minb) ib = minb;
+    return bits + ib;
+  } else {
+  // lossy (encodef.c:63-90)
+  uint32_t bits = 1;
+  int emax = block_emax(block_absmax(v));
+  uint32_t mp = precision3(emax, cp);
+  uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
+  if (e) {
+    w.put(2 * (uint64_t)e + 1, 1 + kE);
+    bits += kE;
+    fwd_cast(q, v, emax);
+    xform<3, false, false>(q);
+    uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
+    uint32_t ib = encode_ints3(w, q, cp.maxbits - bits, mp);
+    if (ib < minb) ib = minb;
+    bits += ib;
+  } else {
+    w.put(0, 1);
+    if (cp.minbits > bits) bits = cp.minbits;
+  }
+  return bits;
+  }
+}
+
+// Decode one block; returns the number of bits consumed (incl. padding).
+template <typename S, bool REV>
+__device__ __forceinline__ uint32_t decode_block3(WordReader& r, S (&v)[64], const CodecParams& cp)
+{
+  using T = Traits<S>;
+  using Int = typename T::Int;
+  using UInt = typename T::UInt;
+  constexpr uint32_t kE = T::kEbits;
+  Int q[64];
+  if constexpr (REV) {
+    uint32_t bits = 1;
+    if (!r.read1()) {
+#pragma unroll
+      for (int i = 0; i < 64; i++) v[i] = 0;
+      if (cp.minbits > bits) {
+        r.skip(cp.minbits - bits);
+        bits = cp.minbits;
+      }
+      return bits;
+    }
+    bits++;
+    bool reinterp = r.read1() != 0;
+    int emax = 0;
+    if (!reinterp) {
+      bits += kE;
+      emax = (int)r.read(kE) - T::kEbias;
+    }
+    uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
+    uint32_t maxb = cp.maxbits - bits;
+    uint32_t prec = (uint32_t)r.read(T::kPbits) + 1;
+    uint32_t ib = T::kPbits + decode_ints3(r, q, maxb - T::kPbits, prec);
+    if (ib < minb) {
+      r.skip(minb - ib);
+      ib = minb;
+    }
+    xform<3, true, true>(q);
+    if (reinterp) {
+#pragma unroll
+      for (int i = 0; i < 64; i++) {
+        Int x = q[i] < 0 ? (Int)((UInt)q[i] ^ T::kTcMask) : q[i];
+        if constexpr (sizeof(S) == 4)
+          v[i] = __uint_as_float((uint32_t)x);
+        else
+          v[i] = __longlong_as_double((long long)x);
+      }
+    } else if (emax != -T::kEbias) {
+      inv_cast(v, q, emax);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; i++) v[i] = 0;
+    }
+    return bits + ib;
+  } else {
+  uint32_t bits = 1;
+  if (r.read1()) {
+    bits += kE;
+    int emax = (int)r.read(kE) - T::kEbias;
+    uint32_t mp = precision3(emax, cp);
+    uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
+    uint32_t ib = decode_ints3(r, q, cp.maxbits - bits, mp);
+    if (ib < minb) {
+      r.skip(minb - ib);
+      ib = minb;
+    }
+    bits += ib;
+    xform<3, true, false>(q);
+    inv_cast(v, q, emax);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; i++) v[i] = 0;
+    if (cp.minbits > bits) {
+      r.skip(cp.minbits - bits);
+      bits = cp.minbits;
+    }
+  }
+  return bits;
+  }
+}
+
+}  // namespace zfp_amd

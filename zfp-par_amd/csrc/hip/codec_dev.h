@@ -1,0 +1,509 @@
+// Device-side building blocks of the zfp block codec for gfx950 (CDNA4).
+//
+// One 4x4x4 block per lane: the block lives in VGPRs (64 scalars), the
+// lifting transform runs on registers, bit planes come from in-register bit
+// matrix transposes, and the embedded coder writes each lane's bits into a
+// per-lane LDS slot that the wave later packs into the stream.
+//
+// Bit-exactness notes (reference behaviour being reproduced, x86 + glibc):
+//  * block max ignores NaN (`max < |x|`), encodef.c:31-40;
+//  * glibc frexp of +inf stores exponent 0 -> emax = 0;
+//  * the cast scale 2^(intprec-2-emax) overflows to +inf for subnormal-max
+//    blocks (ldexp), and C's float->int conversion yields INT_MIN for NaN and
+//    for |y| >= 2^(intprec-1) (x86 cvtt "integer indefinite") -- the GPU
+//    conversion saturates instead, so it is wrapped in an explicit select.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "zfp_perm_dev.h"
+
+namespace zfp_amd {
+
+constexpr int kMinExp = -1074;  // zfp.h:21
+
+template <typename S>
+struct Traits;
+
+template <>
+struct Traits<float> {
+  using Int = int32_t;
+  using UInt = uint32_t;
+  static constexpr int kEbits = 8;
+  static constexpr int kPbits = 5;
+  static constexpr int kEbias = 127;
+  static constexpr int kIntPrec = 32;
+  static constexpr UInt kNbMask = 0xaaaaaaaau;
+  static constexpr UInt kTcMask = 0x7fffffffu;
+};
+
+template <>
+struct Traits<double> {
+  using Int = int64_t;
+  using UInt = uint64_t;
+  static constexpr int kEbits = 11;
+  static constexpr int kPbits = 6;
+  static constexpr int kEbias = 1023;
+  static constexpr int kIntPrec = 64;
+  static constexpr UInt kNbMask = 0xaaaaaaaaaaaaaaaaull;
+  static constexpr UInt kTcMask = 0x7fffffffffffffffull;
+};
+
+struct CodecParams {
+  uint32_t minbits, maxbits, maxprec;
+  int32_t minexp;
+};
+
+__device__ __forceinline__ uint64_t low_mask(uint32_t n)
+{
+  return n >= 64 ? ~0ull : ((1ull << n) - 1);
+}
+
+__device__ __forceinline__ uint32_t ctz64(uint64_t x)
+{
+  return x ? (uint32_t)__builtin_ctzll(x) : 64u;
+}
+
+// ---------------------------------------------------------------------------
+// Bit writer into a lane's LDS slot (bitstream.inl:289-313 semantics:
+// values appended least-significant bit first, 64-bit little-endian words).
+// ---------------------------------------------------------------------------
+struct SlotWriter {
+  uint64_t* slot;
+  uint64_t acc;
+  uint32_t fill;
+  uint32_t widx;
+
+  __device__ __forceinline__ void init(uint64_t* s)
+  {
+    slot = s;
+    acc = 0;
+    fill = 0;
+    widx = 0;
+  }
+  // v must have no bits at or above n; 0 <= n <= 64
+  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  {
+    acc |= v << fill;
+    uint32_t t = fill + n;
+    if (t >= 64) {
+      slot[widx++] = acc;
+      acc = fill ? (v >> (64 - fill)) : 0ull;
+      t -= 64;
+    }
+    fill = t;
+  }
+  __device__ __forceinline__ uint32_t written() const { return widx * 64 + fill; }
+  // flush the pending partial word (zero padded)
+  __device__ __forceinline__ void finish()
+  {
+    if (fill) {
+      slot[widx++] = acc;
+      acc = 0;
+      fill = 0;
+    }
+  }
+};
+
+// Bit reader over a word array in LDS (or global memory).
+struct WordReader {
+  const uint64_t* w;
+  uint64_t pos;
+
+  __device__ __forceinline__ uint64_t peek64() const
+  {
+    uint64_t i = pos >> 6;
+    uint32_t r = (uint32_t)(pos & 63);
+    uint64_t v = w[i] >> r;
+    if (r)
+      v |= w[i + 1] << (64 - r);
+    return v;
+  }
+  __device__ __forceinline__ uint64_t read(uint32_t n)
+  {
+    uint64_t v = n ? (peek64() & low_mask(n)) : 0ull;
+    pos += n;
+    return v;
+  }
+  __device__ __forceinline__ uint32_t read1()
+  {
+    uint64_t i = pos >> 6;
+    uint32_t r = (uint32_t)(pos & 63);
+    pos++;
+    return (uint32_t)((w[i] >> r) & 1u);
+  }
+  __device__ __forceinline__ void skip(uint64_t n) { pos += n; }
+};
+
+// ---------------------------------------------------------------------------
+// Exponents and casts (encodef.c:11-59, codecf.c:17-32)
+// ---------------------------------------------------------------------------
+template <int N>
+__device__ __forceinline__ float block_absmax(const float (&v)[N])
+{
+  float m = 0.0f;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    float a = fabsf(v[i]);
+    m = (m < a) ? a : m;  // NaN never wins
+  }
+  return m;
+}
+
+template <int N>
+__device__ __forceinline__ double block_absmax(const double (&v)[N])
+{
+  double m = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    double a = fabs(v[i]);
+    m = (m < a) ? a : m;
+  }
+  return m;
+}
+
+// exponent(): frexp exponent of the max, clamped to 1-EBIAS; 0 -> -EBIAS.
+// glibc's frexp stores 0 for +-inf at run time (checked against the reference
+// build; a compile-time-folded frexp would leave it untouched instead), so an
+// inf-max block gets emax = 0.
+__device__ __forceinline__ int block_emax(float m)
+{
+  uint32_t b = __float_as_uint(m);
+  if (b == 0)
+    return -127;
+  int be = (int)(b >> 23);
+  if (be == 255)
+    return 0;
+  if (be == 0)
+    return -126;
+  return be - 126;
+}
+
+__device__ __forceinline__ int block_emax(double m)
+{
+  uint64_t b = (uint64_t)__double_as_longlong(m);
+  if (b == 0)
+    return -1023;
+  int be = (int)(b >> 52);
+  if (be == 2047)
+    return 0;
+  if (be == 0)
+    return -1022;
+  return be - 1022;
+}
+
+// exact ldexp(1, e) in the scalar type, with IEEE overflow to +inf and
+// gradual underflow (subnormal powers of two) then zero
+__device__ __forceinline__ float pow2f(int e)
+{
+  if (e > 127)
+    return __uint_as_float(0x7f800000u);
+  if (e >= -126)
+    return __uint_as_float((uint32_t)(e + 127) << 23);
+  if (e >= -149)
+    return __uint_as_float(1u << (e + 149));
+  return 0.0f;
+}
+
+__device__ __forceinline__ double pow2d(int e)
+{
+  if (e > 1023)
+    return __longlong_as_double(0x7ff0000000000000ll);
+  if (e >= -1022)
+    return __longlong_as_double((long long)((uint64_t)(e + 1023) << 52));
+  if (e >= -1074)
+    return __longlong_as_double((long long)(1ull << (e + 1074)));
+  return 0.0;
+}
+
+// (Int)(s * x) with x86 semantics: NaN / out of range -> INT_MIN
+__device__ __forceinline__ int32_t cast_trunc(float y)
+{
+  return (fabsf(y) < 2147483648.0f) ? (int32_t)y : (int32_t)0x80000000u;
+}
+
+__device__ __forceinline__ int64_t cast_trunc(double y)
+{
+  return (fabs(y) < 9223372036854775808.0) ? (int64_t)y : (int64_t)0x8000000000000000ull;
+}
+
+template <int N>
+__device__ __forceinline__ void fwd_cast(int32_t (&q)[N], const float (&v)[N], int emax)
+{
+  float s = pow2f(30 - emax);
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    q[i] = cast_trunc(s * v[i]);
+}
+
+template <int N>
+__device__ __forceinline__ void fwd_cast(int64_t (&q)[N], const double (&v)[N], int emax)
+{
+  double s = pow2d(62 - emax);
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    q[i] = cast_trunc(s * v[i]);
+}
+
+template <int N>
+__device__ __forceinline__ void inv_cast(float (&v)[N], const int32_t (&q)[N], int emax)
+{
+  float s = pow2f(emax - 30);
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    v[i] = s * (float)q[i];
+}
+
+template <int N>
+__device__ __forceinline__ void inv_cast(double (&v)[N], const int64_t (&q)[N], int emax)
+{
+  double s = pow2d(emax - 62);
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    v[i] = s * (double)q[i];
+}
+
+__device__ __forceinline__ uint32_t bits_of(float x) { return __float_as_uint(x); }
+__device__ __forceinline__ uint64_t bits_of(double x) { return (uint64_t)__double_as_longlong(x); }
+
+// ---------------------------------------------------------------------------
+// Lifting (encode.c:31-56, decode.c:9-34, revencode.c:7-30, revdecode.c:7-29)
+// Arithmetic is done on the unsigned type to get the reference's wrap-around.
+// ---------------------------------------------------------------------------
+template <typename Int>
+struct Lift {
+  using U = typename std::make_unsigned<Int>::type;
+  static __device__ __forceinline__ Int add(Int a, Int b) { return (Int)((U)a + (U)b); }
+  static __device__ __forceinline__ Int sub(Int a, Int b) { return (Int)((U)a - (U)b); }
+  static __device__ __forceinline__ Int shl1(Int a) { return (Int)((U)a << 1); }
+
+  static __device__ __forceinline__ void fwd(Int& x, Int& y, Int& z, Int& w)
+  {
+    x = add(x, w); x >>= 1; w = sub(w, x);
+    z = add(z, y); z >>= 1; y = sub(y, z);
+    x = add(x, z); x >>= 1; z = sub(z, x);
+    w = add(w, y); w >>= 1; y = sub(y, w);
+    w = add(w, y >> 1); y = sub(y, w >> 1);
+  }
+  static __device__ __forceinline__ void inv(Int& x, Int& y, Int& z, Int& w)
+  {
+    y = add(y, w >> 1); w = sub(w, y >> 1);
+    y = add(y, w); w = shl1(w); w = sub(w, y);
+    z = add(z, x); x = shl1(x); x = sub(x, z);
+    y = add(y, z); z = shl1(z); z = sub(z, y);
+    w = add(w, x); x = shl1(x); x = sub(x, w);
+  }
+  static __device__ __forceinline__ void rfwd(Int& x, Int& y, Int& z, Int& w)
+  {
+    w = sub(w, z); z = sub(z, y); y = sub(y, x);
+    w = sub(w, z); z = sub(z, y);
+    w = sub(w, z);
+  }
+  static __device__ __forceinline__ void rinv(Int& x, Int& y, Int& z, Int& w)
+  {
+    w = add(w, z);
+    z = add(z, y); w = add(w, z);
+    y = add(y, x); z = add(z, y); w = add(w, z);
+  }
+};
+
+// Separable transform of a 4^D block held in registers; axis order x,y,z(,w)
+// forward and reversed for the inverse (encode3.c:35-49, decode3.c:27-42 and
+// the 4D twins).  All indices are compile-time after unrolling.
+template <int D, bool INV, bool REV, typename Int>
+__device__ __forceinline__ void xform(Int (&p)[1 << (2 * D)])
+{
+  constexpr int N = 1 << (2 * D);
+#pragma unroll
+  for (int step = 0; step < D; step++) {
+    const int axis = INV ? D - 1 - step : step;
+    const int s = 1 << (2 * axis);
+#pragma unroll
+    for (int base = 0; base < N; base++) {
+      if ((base >> (2 * axis)) & 3)
+        continue;
+      Int& x = p[base];
+      Int& y = p[base + s];
+      Int& z = p[base + 2 * s];
+      Int& w = p[base + 3 * s];
+      if (REV) {
+        if (INV) Lift<Int>::rinv(x, y, z, w);
+        else Lift<Int>::rfwd(x, y, z, w);
+      } else {
+        if (INV) Lift<Int>::inv(x, y, z, w);
+        else Lift<Int>::fwd(x, y, z, w);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Bit-matrix transpose of 32x32 bits held in 32 registers: a[r] bit c <-> a[c] bit r.
+// Used both ways: coefficients -> bit planes (encode) and back (decode).
+// ---------------------------------------------------------------------------
+template <int J>
+__device__ __forceinline__ void transpose_step(uint32_t (&a)[32])
+{
+  constexpr uint32_t M = (J == 16) ? 0x0000ffffu : (J == 8) ? 0x00ff00ffu : (J == 4) ? 0x0f0f0f0fu
+                                                 : (J == 2) ? 0x33333333u : 0x55555555u;
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    if (k & J)
+      continue;
+    uint32_t t = ((a[k] >> J) ^ a[k | J]) & M;
+    a[k] ^= t << J;
+    a[k | J] ^= t;
+  }
+}
+
+__device__ __forceinline__ void transpose32(uint32_t (&a)[32])
+{
+  transpose_step<16>(a);
+  transpose_step<8>(a);
+  transpose_step<4>(a);
+  transpose_step<2>(a);
+  transpose_step<1>(a);
+}
+
+// ---------------------------------------------------------------------------
+// Embedded coder for a 64-coefficient block (encode.c:92-256).  Planes are
+// visited MSB first in lock-step across the wave (compile-time plane index,
+// so P[k] stays in registers); per-lane state: remaining budget and the
+// significance count n.  A plane is: the first n bits verbatim, then group
+// tests -- a run "1 0^t 1" per newly significant coefficient (the final
+// coefficient's closing 1 implicit), "0" ends the plane.  The budget may cut a
+// run anywhere: exactly the reference's bit-by-bit truncation.
+// ---------------------------------------------------------------------------
+// one plane of the coder (k is the plane number; P[k] its 64 bits)
+__device__ __forceinline__ void code_plane64(SlotWriter& w, uint64_t plane, uint32_t& bits, uint32_t& n)
+{
+  uint32_t m = n < bits ? n : bits;
+  w.put(plane & low_mask(m), m);
+  bits -= m;
+  uint64_t x = n >= 64 ? 0ull : (plane >> n);
+  while (bits && n < 64) {
+    if (!x) {
+      w.put(0, 1);
+      bits--;
+      break;
+    }
+    uint32_t t = ctz64(x);
+    uint64_t pat;
+    uint32_t len, nn;
+    if (n + t < 63) {
+      pat = 1ull | (1ull << (t + 1));
+      len = t + 2;
+      nn = n + t + 1;
+    } else {
+      pat = 1ull;
+      len = t + 1;
+      nn = 64;
+    }
+    if (len > bits) {
+      len = bits;
+      pat &= low_mask(len);
+    }
+    w.put(pat, len);
+    bits -= len;
+    x = nn >= 64 ? 0ull : (x >> (t + 1));
+    n = nn;
+  }
+}
+
+// compile-time walk over planes K, K-1, ..., 0 so that P[K] is a register
+template <int K, int PREC>
+struct EncodePlanes {
+  static __device__ __forceinline__ void run(SlotWriter& w, const uint64_t (&P)[PREC], uint32_t kmin, uint32_t& bits,
+                                             uint32_t& n)
+  {
+    bool act = bits != 0 && (uint32_t)K >= kmin;
+    if (!__any(act))
+      return;
+    if (act)
+      code_plane64(w, P[K], bits, n);
+    EncodePlanes<K - 1, PREC>::run(w, P, kmin, bits, n);
+  }
+};
+
+template <int PREC>
+struct EncodePlanes<-1, PREC> {
+  static __device__ __forceinline__ void run(SlotWriter&, const uint64_t (&)[PREC], uint32_t, uint32_t&, uint32_t&) {}
+};
+
+template <int PREC>
+__device__ __forceinline__ uint32_t code_planes64(SlotWriter& w, uint32_t budget, uint32_t maxprec,
+                                                  const uint64_t (&P)[PREC])
+{
+  const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
+  uint32_t bits = budget;
+  uint32_t n = 0;
+  EncodePlanes<PREC - 1, PREC>::run(w, P, kmin, bits, n);
+  return budget - bits;
+}
+
+// Decoder twin (decode.c:69-246), including the reference quirk that a
+// positive group test sets the bit where the scan stopped even when the
+// budget ran out first.
+__device__ __forceinline__ uint64_t decode_plane64(WordReader& r, uint32_t& bits, uint32_t& n)
+{
+  uint32_t m = n < bits ? n : bits;
+  uint64_t x = r.read(m);
+  bits -= m;
+  while (bits && n < 64) {
+    bits--;
+    if (!r.read1())
+      break;
+    uint32_t lim = 63 - n;
+    if (lim > bits)
+      lim = bits;
+    uint32_t z = ctz64(r.peek64());
+    if (z < lim) {
+      r.skip(z + 1);
+      bits -= z + 1;
+      n += z;
+    } else {
+      r.skip(lim);
+      bits -= lim;
+      n += lim;
+    }
+    x |= 1ull << n;
+    n++;
+  }
+  return x;
+}
+
+template <int K, int PREC>
+struct DecodePlanes {
+  static __device__ __forceinline__ void run(WordReader& r, uint64_t (&P)[PREC], uint32_t kmin, uint32_t& bits,
+                                             uint32_t& n)
+  {
+    bool act = bits != 0 && (uint32_t)K >= kmin;
+    if (!__any(act))
+      return;
+    if (act)
+      P[K] = decode_plane64(r, bits, n);
+    DecodePlanes<K - 1, PREC>::run(r, P, kmin, bits, n);
+  }
+};
+
+template <int PREC>
+struct DecodePlanes<-1, PREC> {
+  static __device__ __forceinline__ void run(WordReader&, uint64_t (&)[PREC], uint32_t, uint32_t&, uint32_t&) {}
+};
+
+template <int PREC>
+__device__ __forceinline__ uint32_t decode_planes64(WordReader& r, uint32_t budget, uint32_t maxprec,
+                                                    uint64_t (&P)[PREC])
+{
+  const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
+  uint32_t bits = budget;
+  uint32_t n = 0;
+#pragma unroll
+  for (int k = 0; k < PREC; k++)
+    P[k] = 0;
+  DecodePlanes<PREC - 1, PREC>::run(r, P, kmin, bits, n);
+  return budget - bits;
+}
+
+}  // namespace zfp_amd

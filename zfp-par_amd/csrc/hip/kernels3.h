@@ -1,0 +1,370 @@
+// 3D encode/decode kernels: one block per lane, 4 independent waves per
+// 256-thread workgroup, each wave owning 64 consecutive blocks (raster order of
+// the chunk box, compress.c:86-94) and a private LDS region.
+//
+//  encode3_aligned  fixed rate with every block starting on a 64-bit word:
+//                   lane slots in LDS are copied out as one contiguous run.
+//  encode3_general  any mode/alignment: blocks are packed at their bit
+//                   offsets (fixed rate: analytic; variable rate: decoupled
+//                   look-back over per-wave bit totals), interior words are
+//                   plain stores, words shared with a neighbouring wave are
+//                   handed to the fix-up kernels.
+//  decode3          stages the wave's segment of the stream in LDS, then each
+//                   lane decodes its block from its bit offset.
+#pragma once
+
+#include "block3.h"
+
+namespace zfp_amd {
+
+constexpr int kWavesPerGroup = 4;
+constexpr uint64_t kNoWord = ~0ull;
+
+struct Partial {
+  uint64_t idx;  // stream word index relative to the kernel's `out`
+  uint64_t val;
+};
+
+// inclusive prefix sum across the 64 lanes of a wave
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
+{
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t y = __shfl_up(x, d, 64);
+    if (lane >= d) x += y;
+  }
+  return x;
+}
+
+// ---------------------------------------------------------------------------
+// Fixed rate, block size a multiple of 64 bits.  The wave's 64 blocks form one
+// contiguous run of words; with a stream offset r0 = g0 (mod 64) != 0 every
+// output word is a funnel shift of two run words, and the run's first and
+// last words (shared with neighbouring waves) go to the fix-up kernels.
+template <typename S, bool VEC, bool REV>
+__global__ __launch_bounds__(256) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
+                                                       uint64_t* __restrict__ out, uint32_t sw, uint32_t swp,
+                                                       uint32_t r0, Partial* __restrict__ partials)
+{
+  extern __shared__ uint64_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint64_t* wslot = lds + (size_t)wv * 64 * swp;
+  const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  const uint64_t first = w * 64;
+  const uint64_t b = first + lane;
+  SlotWriter wr;
+  wr.init(wslot + (size_t)lane * swp);
+  if (b < g.nblocks) {
+    S v[64];
+    BlockPos p = block_pos(g, b, 3);
+    gather3<S, VEC>(v, data, g, p);
+    encode_block3<S, REV>(wr, v, cp);
+    wr.finish();
+    while (wr.widx < sw)
+      wr.slot[wr.widx++] = 0;
+  }
+  __syncthreads();
+  if (first >= g.nblocks)
+    return;
+  const uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
+  const uint32_t total = (uint32_t)nb * sw;  // run length in words
+  if (r0 == 0) {
+    uint64_t* dst = out + first * sw;
+    for (uint32_t i = lane; i < total; i += 64) {
+      uint32_t l = i / sw;
+      uint32_t k = i - l * sw;
+      dst[i] = wslot[(size_t)l * swp + k];
+    }
+    return;
+  }
+  // run words j = 0..total-1 land at bit r0 + 64 j of out[first*sw ...]
+  uint64_t* dst = out + first * sw;
+  for (uint32_t j = lane; j <= total; j += 64) {
+    uint64_t cur = 0, prev = 0;
+    if (j < total) {
+      uint32_t l = j / sw;
+      cur = wslot[(size_t)l * swp + (j - l * sw)];
+    }
+    if (j > 0) {
+      uint32_t l = (j - 1) / sw;
+      prev = wslot[(size_t)l * swp + (j - 1 - l * sw)];
+    }
+    uint64_t val = (cur << r0) | (prev >> (64 - r0));
+    if (j == 0) {
+      partials[2 * w] = Partial{first * sw, val};
+    } else if (j == total) {
+      partials[2 * w + 1] = Partial{first * sw + total, val};
+    } else {
+      dst[j] = val;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Extract `cnt` (<= 64) bits starting at bit `pos` of a lane slot.
+__device__ __forceinline__ uint64_t slot_bits(const uint64_t* slot, uint32_t pos, uint32_t cnt)
+{
+  uint32_t i = pos >> 6, r = pos & 63;
+  uint64_t v = slot[i] >> r;
+  if (r && r + cnt > 64)
+    v |= slot[i + 1] << (64 - r);
+  return v & low_mask(cnt);
+}
+
+struct GeneralArgs {
+  uint64_t* out;          // stream words, index 0 = word containing bit g0
+  uint32_t g0;            // start bit within out[0]
+  uint32_t swp;           // slot stride (words) per lane
+  uint32_t var;           // 1: variable rate (look-back), 0: fixed rate
+  uint32_t maxbits;       // fixed rate block size
+  uint64_t* status;       // per-wave look-back words (zeroed per launch)
+  uint32_t* ticket;       // wave ticket counter (zeroed per launch)
+  Partial* partials;      // 2 per wave
+  uint16_t* idx_len;      // per-block bit lengths (variable rate; optional)
+  uint64_t* idx_base;     // per-wave start offsets relative to g0 (optional)
+  uint64_t* total_bits;   // written by the last wave (variable rate)
+  uint32_t* error;        // look-back timeout flag
+};
+
+constexpr uint64_t kStAgg = 1ull << 62;
+constexpr uint64_t kStIncl = 2ull << 62;
+constexpr uint64_t kStMask = (1ull << 62) - 1;
+
+// Decoupled look-back (single-pass chained scan): each wave publishes its
+// aggregate, walks back over predecessors' status words until an inclusive
+// prefix, publishes its own inclusive prefix.  Status words are the data
+// (one 8-byte agent-scope atomic store/load each), so no separate flag or
+// fence is needed; waves take tickets in launch order so every awaited wave
+// is already running.  Spins are bounded (error flag on timeout).
+__device__ __forceinline__ uint64_t lookback(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
+{
+  uint64_t excl = 0;
+  if (w == 0) {
+    __hip_atomic_store(&status[0], kStIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  __hip_atomic_store(&status[w], kStAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t j = w - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    uint64_t st = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t tag = st & ~kStMask;
+    if (tag == 0) {
+      if (++spins > (1u << 26)) {
+        atomicOr(error, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += st & kStMask;
+    if (tag == kStIncl || j == 0)
+      break;
+    j--;
+  }
+  __hip_atomic_store(&status[w], kStIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+template <typename S, bool VEC, bool REV>
+__global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ data, Geometry g, CodecParams cp,
+                                                       GeneralArgs a)
+{
+  extern __shared__ uint64_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  // per wave: 64 slots, then 64 offsets + 64 written counts (uint32)
+  uint64_t* wbase = lds + (size_t)wv * (64 * a.swp + 64);
+  uint32_t* off = reinterpret_cast<uint32_t*>(wbase + 64 * a.swp);
+  uint32_t* wrt = off + 64;
+
+  const uint64_t nwaves = (g.nblocks + 63) / 64;
+  uint64_t w;
+  if (a.var) {
+    uint32_t t = 0;
+    if (lane == 0)
+      t = atomicAdd(a.ticket, 1u);
+    w = (uint64_t)__shfl(t, 0, 64);
+  } else {
+    w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  }
+  const bool live = w < nwaves;
+  const uint64_t first = w * 64;
+  const uint64_t b = first + lane;
+
+  SlotWriter wr;
+  wr.init(wbase + (size_t)lane * a.swp);
+  uint32_t len = 0;
+  if (live && b < g.nblocks) {
+    S v[64];
+    BlockPos p = block_pos(g, b, 3);
+    gather3<S, VEC>(v, data, g, p);
+    len = encode_block3<S, REV>(wr, v, cp);
+    wr.finish();
+  }
+  const uint32_t incl = wave_incl_scan(len);
+  const uint32_t excl_l = incl - len;
+  const uint32_t total = __shfl(incl, 63, 64);
+  off[lane] = excl_l;
+  wrt[lane] = b < g.nblocks ? (wr.widx * 64 < len ? wr.widx * 64 : len) : 0;
+
+  uint64_t start = 0;  // bit offset of the wave's first block relative to g0
+  if (!live) {
+  } else if (a.var) {
+    uint64_t e = 0;
+    if (lane == 0)
+      e = lookback(a.status, w, total, a.error);
+    start = __shfl(e, 0, 64);
+    if (a.idx_len && b < g.nblocks)
+      a.idx_len[b] = (uint16_t)len;
+    if (lane == 0) {
+      if (a.idx_base)
+        a.idx_base[w] = start;
+      if (w == nwaves - 1)
+        *a.total_bits = start + total;
+    }
+  } else {
+    start = first * (uint64_t)a.maxbits;
+  }
+  __syncthreads();
+  if (!live)
+    return;
+
+  // gather stream words of [G, G + total), G = g0 + start
+  const uint64_t G = a.g0 + start;
+  const uint64_t W0 = G >> 6;
+  const uint32_t r0 = (uint32_t)(G & 63);
+  const uint64_t end = G + total;
+  const uint64_t W1 = (end - 1) >> 6;
+  const uint32_t nw = (uint32_t)(W1 - W0 + 1);
+  for (uint32_t o = lane; o < nw; o += 64) {
+    // local bit range of this word relative to the wave's first bit
+    int64_t lo = (int64_t)o * 64 - r0;
+    int64_t hi = lo + 64;
+    // first lane whose block ends after lo
+    int l = 0;
+    {
+      int lo_i = 0, hi_i = 63;
+      int64_t key = lo < 0 ? 0 : lo;
+      while (lo_i < hi_i) {
+        int mid = (lo_i + hi_i + 1) >> 1;
+        if ((int64_t)off[mid] <= key) lo_i = mid;
+        else hi_i = mid - 1;
+      }
+      l = lo_i;
+    }
+    uint64_t val = 0;
+    for (; l < 64 && (int64_t)off[l] < hi; l++) {
+      int64_t s0 = off[l];
+      int64_t s1 = s0 + wrt[l];
+      int64_t x0 = s0 > lo ? s0 : lo;
+      int64_t x1 = s1 < hi ? s1 : hi;
+      if (x0 < x1)
+        val |= slot_bits(wbase + (size_t)l * a.swp, (uint32_t)(x0 - s0), (uint32_t)(x1 - x0)) << (x0 - lo);
+    }
+    bool head = (o == 0) && (r0 != 0 || (nw == 1 && (end & 63)));
+    bool tail = (o == nw - 1) && (end & 63);
+    if (head || tail) {
+      Partial pr;
+      pr.idx = W0 + o;
+      pr.val = val;
+      a.partials[2 * w + (o == 0 ? 0 : 1)] = pr;
+    } else {
+      a.out[W0 + o] = val;
+    }
+  }
+  if (lane == 0) {
+    bool head = r0 != 0 || (nw == 1 && (end & 63));
+    bool tail = (end & 63) != 0;
+    if (!head)
+      a.partials[2 * w].idx = kNoWord;
+    if (!tail || nw == 1)
+      a.partials[2 * w + 1].idx = kNoWord;
+  }
+}
+
+// Zero every word that receives partial contributions (the word holding the
+// stream's pending bits below g0 gets those bits instead), then OR them in.
+__global__ void fixup_zero(const Partial* __restrict__ partials, uint64_t n, uint64_t* out, uint64_t head_idx,
+                           uint64_t head_val)
+{
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  uint64_t idx = partials[i].idx;
+  if (idx != kNoWord)
+    out[idx] = (idx == head_idx) ? head_val : 0ull;
+}
+
+__global__ void fixup_or(const Partial* __restrict__ partials, uint64_t n, uint64_t* out)
+{
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n)
+    return;
+  Partial p = partials[i];
+  if (p.idx != kNoWord)
+    atomicOr((unsigned long long*)&out[p.idx], (unsigned long long)p.val);
+}
+
+// ---------------------------------------------------------------------------
+struct DecodeArgs {
+  const uint64_t* in;      // stream words, index 0 = word containing bit g0
+  uint64_t in_words;       // readable words from `in`
+  uint32_t g0;
+  uint32_t var;
+  uint32_t maxbits;
+  uint32_t seg_words;      // LDS words per wave
+  const uint16_t* idx_len;
+  const uint64_t* idx_base;
+};
+
+template <typename S, bool VEC, bool REV>
+__global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
+{
+  extern __shared__ uint64_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint64_t* seg = lds + (size_t)wv * a.seg_words;
+  const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  const uint64_t first = w * 64;
+  const bool live = first < g.nblocks;
+  const uint64_t b = first + lane;
+  const bool act = b < g.nblocks;
+
+  uint64_t start = 0;
+  uint32_t pos = 0, total = 0;
+  if (!live) {
+  } else if (a.var) {
+    uint32_t len = act ? a.idx_len[b] : 0u;
+    uint32_t incl = wave_incl_scan(len);
+    pos = incl - len;
+    total = __shfl(incl, 63, 64);
+    start = a.idx_base[w];
+  } else {
+    uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
+    pos = lane * a.maxbits;
+    total = (uint32_t)nb * a.maxbits;
+    start = first * (uint64_t)a.maxbits;
+  }
+  const uint64_t G = a.g0 + start;
+  const uint64_t W0 = G >> 6;
+  const uint32_t nw = (uint32_t)(((G + total + 63) >> 6) - W0 + 1);
+  for (uint32_t o = lane; live && o < nw && o < a.seg_words; o += 64) {
+    uint64_t gi = W0 + o;
+    seg[o] = gi < a.in_words ? a.in[gi] : 0ull;
+  }
+  __syncthreads();
+  if (!act)
+    return;
+  WordReader r;
+  r.w = seg;
+  r.pos = (G & 63) + pos;
+  S v[64];
+  decode_block3<S, REV>(r, v, cp);
+  BlockPos p = block_pos(g, b, 3);
+  scatter3<S, VEC>(v, data, g, p);
+}
+
+}  // namespace zfp_amd

@@ -1,0 +1,640 @@
+// libzfp_hip.so -- MI355X codec library behind include/zfp_hip.h.
+//
+// Host side of the C-ABI: validates a job, works out where the field and the
+// stream live (host or device), stages host buffers through per-thread device
+// scratch on a per-thread HIP stream, picks a kernel path and launches it.
+//
+//   fixed rate, block size a multiple of 64 bits  -> encode3_aligned (+ one
+//        funnel-shift pass when the stream offset is not word aligned)
+//   everything else (variable rate, odd block sizes) -> encode3_general with
+//        decoupled look-back, then fixup_zero/fixup_or for words shared by waves
+//   decode: decode3 (fixed-rate offsets analytic, variable rate from the index)
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "kernels3.h"
+#include "zfp_hip.h"
+
+using namespace zfp_amd;
+
+// ---------------------------------------------------------------------------
+// errors
+static thread_local std::string g_err;
+
+static int fail(const char* fmt, ...)
+{
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return 0;
+}
+
+#define HIP_TRY(expr)                                                                   \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail("%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, __LINE__); \
+  } while (0)
+
+// ---------------------------------------------------------------------------
+// block index (variable-rate streams)
+struct zfp_hip_index {
+  int device = -1;
+  uint64_t nblocks = 0;
+  uint64_t nwaves = 0;
+  uint64_t total_bits = 0;
+  uint16_t* d_len = nullptr;   // per-block bit length
+  uint64_t* d_base = nullptr;  // per-wave start bit relative to the stream's first block
+  size_t cap_blocks = 0, cap_waves = 0;
+};
+
+// ---------------------------------------------------------------------------
+// per-thread, per-device context
+struct Scratch {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+struct Ctx {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  Scratch field, words, status, partials, misc;
+  double kernel_ms = 0, total_ms = 0;
+  bool timed = false;
+};
+
+static thread_local std::vector<Ctx*> t_ctx;
+static thread_local Ctx* t_last = nullptr;
+
+static int ensure(Scratch& s, size_t bytes)
+{
+  if (s.bytes >= bytes)
+    return 1;
+  if (s.p)
+    (void)hipFree(s.p);
+  s.p = nullptr;
+  s.bytes = 0;
+  size_t want = std::max(bytes, (size_t)4096);
+  hipError_t e = hipMalloc(&s.p, want);
+  if (e != hipSuccess)
+    return fail("hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+  s.bytes = want;
+  return 1;
+}
+
+static Ctx* get_ctx(int device)
+{
+  if (device < 0) {
+    if (hipGetDevice(&device) != hipSuccess)
+      device = 0;
+  }
+  for (Ctx* c : t_ctx)
+    if (c->device == device) {
+      (void)hipSetDevice(device);
+      return c;
+    }
+  if (hipSetDevice(device) != hipSuccess) {
+    fail("hipSetDevice(%d) failed", device);
+    return nullptr;
+  }
+  Ctx* c = new Ctx;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    fail("hipStreamCreate failed");
+    delete c;
+    return nullptr;
+  }
+  for (auto& e : c->ev)
+    (void)hipEventCreate(&e);
+  t_ctx.push_back(c);
+  return c;
+}
+
+static bool is_device_ptr(const void* p)
+{
+  if (!p)
+    return false;
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return attr.type == hipMemoryTypeDevice;
+}
+
+// ---------------------------------------------------------------------------
+// job analysis
+struct Plan {
+  int dims = 0;
+  bool dbl = false;
+  Geometry g{};
+  CodecParams cp{};
+  bool fixed = false;        // every block exactly maxbits bits
+  bool vec = false;          // 16-byte row loads/stores possible
+  uint32_t bound_bits = 0;   // max bits a block writes (excl. padding)
+  uint32_t max_len = 0;      // max block length incl. padding
+  int64_t span_lo = 0, span_hi = 0;  // element offsets touched by the box
+};
+
+static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
+{
+  if (!j)
+    return fail("null job");
+  if (j->type != 3 && j->type != 4)
+    return fail("zfp_hip: scalar type %d not supported (float and double only)", j->type);
+  if (j->dims != 3)
+    return fail("zfp_hip: %dD fields not supported yet (3D only)", j->dims);
+  p.dims = j->dims;
+  p.dbl = j->type == 4;
+  p.cp.minbits = j->minbits;
+  p.cp.maxbits = j->maxbits;
+  p.cp.maxprec = j->maxprec;
+  p.cp.minexp = j->minexp;
+  if (p.cp.maxprec == 0 || p.cp.maxprec > 64)
+    return fail("zfp_hip: invalid maxprec %u", p.cp.maxprec);
+  p.g.nblocks = 1;
+  p.span_lo = p.span_hi = 0;
+  for (int a = 0; a < 4; a++) {
+    p.g.n[a] = a < p.dims ? j->n[a] : 1;
+    p.g.s[a] = a < p.dims ? j->s[a] : 0;
+    p.g.f[a] = a < p.dims ? j->f[a] : 0;
+    uint64_t e = a < p.dims ? j->e[a] : 1;
+    uint64_t nb = (a < p.dims) ? (e > p.g.f[a] ? (e - p.g.f[a] + 3) / 4 : 0) : 1;
+    if (a < p.dims && e > p.g.n[a])
+      return fail("zfp_hip: chunk end %llu exceeds field extent %llu on axis %d", (unsigned long long)e,
+                  (unsigned long long)p.g.n[a], a);
+    if (nb > 0xffffffffull)
+      return fail("zfp_hip: too many blocks along axis %d", a);
+    p.g.nb[a] = (uint32_t)nb;
+    p.g.nblocks *= nb;
+    if (a < p.dims && e > p.g.f[a]) {
+      int64_t d0 = (int64_t)p.g.f[a] * p.g.s[a];
+      int64_t d1 = (int64_t)(e - 1) * p.g.s[a];
+      p.span_lo += std::min(d0, d1);
+      p.span_hi += std::max(d0, d1);
+    }
+  }
+  const int ebits = p.dbl ? 11 : 8, pbits = p.dbl ? 6 : 5, intprec = p.dbl ? 64 : 32;
+  const bool rev = p.cp.minexp < kMinExp;
+  const uint32_t hdr = rev ? 2 + ebits + pbits : 1 + ebits;
+  uint64_t body = hdr + 63 + 64ull * std::min<uint32_t>(p.cp.maxprec, intprec);
+  uint64_t bound = body;
+  if (p.cp.maxbits >= hdr)
+    bound = std::min<uint64_t>(bound, p.cp.maxbits);
+  p.bound_bits = (uint32_t)bound;
+  p.max_len = std::max<uint32_t>(p.bound_bits, p.cp.minbits);
+  p.fixed = !rev && p.cp.minbits == p.cp.maxbits && p.cp.maxbits >= (uint32_t)(1 + ebits);
+  const size_t es = p.dbl ? 8 : 4;
+  p.vec = p.g.s[0] == 1 && (p.g.s[1] % 4) == 0 && (p.g.s[2] % 4) == 0 && (p.g.f[0] % 4) == 0 &&
+          ((uintptr_t)field_base % (4 * es)) == 0;
+  return 1;
+}
+
+static size_t slot_words_odd(uint32_t bits)
+{
+  size_t w = (bits + 63) / 64 + 1;
+  return w | 1;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+template <typename S>
+static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out, uint32_t g0,
+                         uint64_t head_word, zfp_hip_index* index, uint64_t* total_bits)
+{
+  const uint64_t nwaves = (p.g.nblocks + 63) / 64;
+  const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
+  if (ngroups > 0x7fffffffull)
+    return fail("zfp_hip: field too large for one launch");
+  dim3 grid((unsigned)ngroups), block(256);
+  if (p.fixed && (p.cp.maxbits % 64) == 0) {
+    const uint32_t sw = p.cp.maxbits / 64;
+    const uint32_t swp = sw | 1;
+    size_t lds = (size_t)kWavesPerGroup * 64 * swp * 8;
+    if (lds > 160 * 1024)
+      return fail("zfp_hip: block size %u bits too large for LDS", p.cp.maxbits);
+    Partial* parts = nullptr;
+    if (g0) {
+      if (!ensure(c->partials, nwaves * 2 * sizeof(Partial)))
+        return 0;
+      parts = (Partial*)c->partials.p;
+    }
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    if (p.vec)
+      hipLaunchKernelGGL((encode3_aligned<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, d_out,
+                         sw, swp, g0, parts);
+    else
+      hipLaunchKernelGGL((encode3_aligned<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, d_out,
+                         sw, swp, g0, parts);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    if (g0) {
+      unsigned fg = (unsigned)((2 * nwaves + 255) / 256);
+      hipLaunchKernelGGL(fixup_zero, dim3(fg), dim3(256), 0, c->stream, parts, 2 * nwaves, d_out, 0ull, head_word);
+      hipLaunchKernelGGL(fixup_or, dim3(fg), dim3(256), 0, c->stream, parts, 2 * nwaves, d_out);
+      HIP_TRY(hipGetLastError());
+    }
+    *total_bits = p.g.nblocks * (uint64_t)p.cp.maxbits;
+    return 1;
+  }
+  // general path
+  const uint32_t swp = (uint32_t)slot_words_odd(p.bound_bits);
+  size_t lds = (size_t)kWavesPerGroup * (64 * swp + 64) * 8;
+  if (lds > 160 * 1024)
+    return fail("zfp_hip: block bound %u bits too large for LDS", p.bound_bits);
+  const bool var = !p.fixed;
+  // misc: [0] total bits, [1] ticket|error
+  if (!ensure(c->partials, nwaves * 2 * sizeof(Partial)) || !ensure(c->misc, 64) ||
+      (var && !ensure(c->status, nwaves * 8)))
+    return 0;
+  GeneralArgs a{};
+  a.out = d_out;
+  a.g0 = g0;
+  a.swp = swp;
+  a.var = var ? 1 : 0;
+  a.maxbits = p.cp.maxbits;
+  a.status = (uint64_t*)c->status.p;
+  a.total_bits = (uint64_t*)c->misc.p;
+  a.ticket = (uint32_t*)((char*)c->misc.p + 8);
+  a.error = (uint32_t*)((char*)c->misc.p + 12);
+  a.partials = (Partial*)c->partials.p;
+  if (var && index) {
+    if (index->cap_blocks < p.g.nblocks) {
+      if (index->d_len) (void)hipFree(index->d_len);
+      index->d_len = nullptr;
+      HIP_TRY(hipMalloc(&index->d_len, p.g.nblocks * sizeof(uint16_t)));
+      index->cap_blocks = p.g.nblocks;
+    }
+    if (index->cap_waves < nwaves) {
+      if (index->d_base) (void)hipFree(index->d_base);
+      index->d_base = nullptr;
+      HIP_TRY(hipMalloc(&index->d_base, nwaves * sizeof(uint64_t)));
+      index->cap_waves = nwaves;
+    }
+    index->device = c->device;
+    index->nblocks = p.g.nblocks;
+    index->nwaves = nwaves;
+    a.idx_len = index->d_len;
+    a.idx_base = index->d_base;
+  }
+  HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, c->stream));
+  if (var)
+    HIP_TRY(hipMemsetAsync(c->status.p, 0, nwaves * 8, c->stream));
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  const bool rev = p.cp.minexp < kMinExp;
+  if (p.vec && rev)
+    hipLaunchKernelGGL((encode3_general<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (p.vec)
+    hipLaunchKernelGGL((encode3_general<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (rev)
+    hipLaunchKernelGGL((encode3_general<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else
+    hipLaunchKernelGGL((encode3_general<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  unsigned fg = (unsigned)((2 * nwaves + 255) / 256);
+  hipLaunchKernelGGL(fixup_zero, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out, 0ull,
+                     g0 ? head_word : 0ull);
+  hipLaunchKernelGGL(fixup_or, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out);
+  HIP_TRY(hipGetLastError());
+  if (var) {
+    uint64_t host[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(host, c->misc.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((uint32_t)(host[1] >> 32))
+      return fail("zfp_hip: look-back timed out (GPU scheduling anomaly)");
+    *total_bits = host[0];
+    if (index)
+      index->total_bits = host[0];
+  } else {
+    *total_bits = p.g.nblocks * (uint64_t)p.cp.maxbits;
+  }
+  return 1;
+}
+
+template <typename S>
+static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
+                         const zfp_hip_index* index)
+{
+  const uint64_t nwaves = (p.g.nblocks + 63) / 64;
+  const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
+  DecodeArgs a{};
+  a.in = d_in;
+  a.in_words = in_words;
+  a.g0 = g0;
+  a.var = p.fixed ? 0 : 1;
+  a.maxbits = p.cp.maxbits;
+  uint32_t per_block = p.fixed ? p.cp.maxbits : p.max_len;
+  a.seg_words = (uint32_t)((64ull * per_block + 63) / 64 + 2);
+  if (!p.fixed) {
+    a.idx_len = index->d_len;
+    a.idx_base = index->d_base;
+  }
+  size_t lds = (size_t)kWavesPerGroup * a.seg_words * 8;
+  if (lds > 160 * 1024)
+    return fail("zfp_hip: block size too large for LDS staging (%u bits)", per_block);
+  dim3 grid((unsigned)ngroups), block(256);
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  const bool rev = p.cp.minexp < kMinExp;
+  if (p.vec && rev)
+    hipLaunchKernelGGL((decode3<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (p.vec)
+    hipLaunchKernelGGL((decode3<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (rev)
+    hipLaunchKernelGGL((decode3<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else
+    hipLaunchKernelGGL((decode3<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  return 1;
+}
+
+static void record_timing(Ctx* c)
+{
+  float k = 0, t = 0;
+  if (hipEventElapsedTime(&k, c->ev[1], c->ev[2]) == hipSuccess &&
+      hipEventElapsedTime(&t, c->ev[0], c->ev[3]) == hipSuccess) {
+    c->kernel_ms = k;
+    c->total_ms = t;
+    c->timed = true;
+  }
+  t_last = c;
+}
+
+// copy the box of elements between a host field and a device image of its
+// span (device pointer d_base corresponds to host pointer h_base)
+static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es, bool to_host)
+{
+  // whole span contiguous?  (full x/y extents, default strides)
+  const Geometry& g = p.g;
+  bool contiguous = true;
+  int64_t expect = 1;
+  for (int a = 0; a < p.dims; a++) {
+    if (g.s[a] != expect)
+      contiguous = false;
+    expect *= (int64_t)g.n[a];
+  }
+  uint64_t e[4];
+  for (int a = 0; a < 4; a++)
+    e[a] = a < p.dims ? std::min<uint64_t>(g.n[a], g.f[a] + 4ull * g.nb[a]) : 1;
+  bool full_lower = true;
+  for (int a = 0; a < p.dims - 1; a++)
+    if (g.f[a] != 0 || e[a] != g.n[a])
+      full_lower = false;
+  hipMemcpyKind kind = to_host ? hipMemcpyDeviceToHost : hipMemcpyHostToDevice;
+  if ((contiguous && full_lower) || !to_host) {
+    // one copy of the span (reading extra elements is harmless)
+    size_t off = (size_t)p.span_lo * es;
+    size_t bytes = (size_t)(p.span_hi - p.span_lo + 1) * es;
+    if (to_host)
+      HIP_TRY(hipMemcpyAsync((char*)h_base + off, (char*)d_base + off, bytes, kind, c->stream));
+    else
+      HIP_TRY(hipMemcpyAsync((char*)d_base + off, (char*)h_base + off, bytes, kind, c->stream));
+    return 1;
+  }
+  if (g.s[0] != 1)
+    return fail("zfp_hip: host-resident decompression of a non-slab chunk needs unit x stride");
+  // row-wise 2D copies, one per (z, w) slice
+  size_t width = (size_t)(e[0] - g.f[0]) * es;
+  size_t rows = p.dims >= 2 ? (size_t)(e[1] - g.f[1]) : 1;
+  size_t pitch = (size_t)(p.dims >= 2 ? g.s[1] : 1) * es;
+  for (uint64_t w = (p.dims >= 4 ? g.f[3] : 0); w < (p.dims >= 4 ? e[3] : 1); w++)
+    for (uint64_t z = (p.dims >= 3 ? g.f[2] : 0); z < (p.dims >= 3 ? e[2] : 1); z++) {
+      int64_t off = (int64_t)g.f[0] * g.s[0] + (int64_t)(p.dims >= 2 ? g.f[1] : 0) * (p.dims >= 2 ? g.s[1] : 0) +
+                    (int64_t)z * (p.dims >= 3 ? g.s[2] : 0) + (int64_t)w * (p.dims >= 4 ? g.s[3] : 0);
+      HIP_TRY(hipMemcpy2DAsync((char*)h_base + off * (int64_t)es, pitch, (char*)d_base + off * (int64_t)es, pitch,
+                               width, rows, kind, c->stream));
+    }
+  return 1;
+}
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int zfp_hip_device_count(void)
+{
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return n;
+}
+
+const char* zfp_hip_last_error(void) { return g_err.c_str(); }
+
+int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* words, uint64_t capacity_words,
+                     uint64_t bit_offset, uint64_t head_word, int device, zfp_hip_index* index, uint64_t* end_bit)
+{
+  Plan p;
+  if (!plan_job(job, field_base, p))
+    return 0;
+  if (!field_base || !words)
+    return fail("zfp_hip_compress: null field or stream pointer");
+  if (zfp_hip_device_count() <= 0)
+    return fail("zfp_hip_compress: no HIP device available");
+  Ctx* c = get_ctx(device);
+  if (!c)
+    return 0;
+  const size_t es = p.dbl ? 8 : 4;
+  const uint64_t W0 = bit_offset >> 6;
+  const uint32_t g0 = (uint32_t)(bit_offset & 63);
+  if (p.g.nblocks == 0) {
+    *end_bit = bit_offset;
+    return 1;
+  }
+  const uint64_t worst_bits = (uint64_t)g0 + p.g.nblocks * (uint64_t)(p.fixed ? p.cp.maxbits : p.max_len);
+  const uint64_t worst_words = (worst_bits + 63) / 64 + 1;
+  const bool dev_field = is_device_ptr(field_base);
+  const bool dev_stream = is_device_ptr(words);
+  if (p.fixed && W0 + (worst_bits + 63) / 64 > capacity_words)
+    return fail("zfp_hip_compress: stream capacity %llu words < %llu needed", (unsigned long long)capacity_words,
+                (unsigned long long)(W0 + (worst_bits + 63) / 64));
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  // field
+  const void* d_field = field_base;
+  if (!dev_field) {
+    size_t bytes = (size_t)(p.span_hi - p.span_lo + 1) * es;
+    if (!ensure(c->field, bytes))
+      return 0;
+    char* d_img = (char*)c->field.p - p.span_lo * (int64_t)es;
+    if (!copy_box(c, p, (void*)field_base, d_img, es, false))
+      return 0;
+    d_field = d_img;
+  }
+  // stream
+  uint64_t* d_out;
+  const bool direct = dev_stream && W0 + worst_words <= capacity_words;
+  if (direct) {
+    d_out = words + W0;
+  } else {
+    if (!ensure(c->words, worst_words * 8))
+      return 0;
+    d_out = (uint64_t*)c->words.p;
+  }
+  uint64_t total = 0;
+  int ok = p.dbl ? launch_encode<double>(c, p, (const double*)d_field, d_out, g0, head_word, index, &total)
+                 : launch_encode<float>(c, p, (const float*)d_field, d_out, g0, head_word, index, &total);
+  if (!ok)
+    return 0;
+  const uint64_t end = bit_offset + total;
+  const uint64_t nwords = (g0 + total + 63) / 64;
+  if (W0 + nwords > capacity_words)
+    return fail("zfp_hip_compress: compressed stream (%llu words) exceeds capacity %llu",
+                (unsigned long long)(W0 + nwords), (unsigned long long)capacity_words);
+  if (!direct) {
+    hipMemcpyKind kind = dev_stream ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    HIP_TRY(hipMemcpyAsync(words + W0, d_out, nwords * 8, kind, c->stream));
+  }
+  HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  record_timing(c);
+  *end_bit = end;
+  return 1;
+}
+
+int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t* words, uint64_t capacity_words,
+                       uint64_t bit_offset, int device, const zfp_hip_index* index, uint64_t* end_bit)
+{
+  Plan p;
+  if (!plan_job(job, field_base, p))
+    return 0;
+  if (!field_base || !words)
+    return fail("zfp_hip_decompress: null field or stream pointer");
+  if (zfp_hip_device_count() <= 0)
+    return fail("zfp_hip_decompress: no HIP device available");
+  if (!p.fixed) {
+    if (!index || !index->d_len || index->nblocks != p.g.nblocks)
+      return fail("zfp_hip_decompress: variable-rate stream needs the block index produced by its compression");
+  }
+  Ctx* c = get_ctx(device);
+  if (!c)
+    return 0;
+  if (!p.fixed && index->device != c->device)
+    return fail("zfp_hip_decompress: block index lives on device %d, decoding on %d", index->device, c->device);
+  const size_t es = p.dbl ? 8 : 4;
+  const uint64_t W0 = bit_offset >> 6;
+  const uint32_t g0 = (uint32_t)(bit_offset & 63);
+  if (p.g.nblocks == 0) {
+    *end_bit = bit_offset;
+    return 1;
+  }
+  const uint64_t total = p.fixed ? p.g.nblocks * (uint64_t)p.cp.maxbits : index->total_bits;
+  const uint64_t nwords = std::min<uint64_t>((g0 + total + 63) / 64 + 1, capacity_words > W0 ? capacity_words - W0 : 0);
+  const bool dev_field = is_device_ptr(field_base);
+  const bool dev_stream = is_device_ptr(words);
+  HIP_TRY(hipEventRecord(c->ev[0], c->stream));
+  const uint64_t* d_in = words + W0;
+  if (!dev_stream) {
+    if (!ensure(c->words, nwords * 8 + 8))
+      return 0;
+    HIP_TRY(hipMemcpyAsync(c->words.p, words + W0, nwords * 8, hipMemcpyHostToDevice, c->stream));
+    d_in = (const uint64_t*)c->words.p;
+  }
+  void* d_field = field_base;
+  char* d_img = nullptr;
+  if (!dev_field) {
+    size_t bytes = (size_t)(p.span_hi - p.span_lo + 1) * es;
+    if (!ensure(c->field, bytes))
+      return 0;
+    d_img = (char*)c->field.p - p.span_lo * (int64_t)es;
+    d_field = d_img;
+  }
+  int ok = p.dbl ? launch_decode<double>(c, p, (double*)d_field, d_in, nwords, g0, index)
+                 : launch_decode<float>(c, p, (float*)d_field, d_in, nwords, g0, index);
+  if (!ok)
+    return 0;
+  if (!dev_field && !copy_box(c, p, field_base, d_img, es, true))
+    return 0;
+  HIP_TRY(hipEventRecord(c->ev[3], c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  record_timing(c);
+  *end_bit = bit_offset + total;
+  return 1;
+}
+
+zfp_hip_index* zfp_hip_index_create(void) { return new zfp_hip_index; }
+
+void zfp_hip_index_free(zfp_hip_index* index)
+{
+  if (!index)
+    return;
+  if (index->d_len) (void)hipFree(index->d_len);
+  if (index->d_base) (void)hipFree(index->d_base);
+  delete index;
+}
+
+uint64_t zfp_hip_index_blocks(const zfp_hip_index* index) { return index ? index->nblocks : 0; }
+
+size_t zfp_hip_index_export(const zfp_hip_index* index, void* buffer, size_t capacity)
+{
+  if (!index)
+    return 0;
+  size_t need = 32 + index->nblocks * 2 + index->nwaves * 8;
+  if (!buffer)
+    return need;
+  if (capacity < need)
+    return 0;
+  uint64_t* h = (uint64_t*)buffer;
+  h[0] = 0x7a6678646e69ull;  // tag
+  h[1] = index->nblocks;
+  h[2] = index->nwaves;
+  h[3] = index->total_bits;
+  char* q = (char*)buffer + 32;
+  if (index->nblocks && hipMemcpy(q, index->d_len, index->nblocks * 2, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  q += index->nblocks * 2;
+  if (index->nwaves && hipMemcpy(q, index->d_base, index->nwaves * 8, hipMemcpyDeviceToHost) != hipSuccess)
+    return 0;
+  return need;
+}
+
+zfp_hip_index* zfp_hip_index_import(const void* buffer, size_t bytes)
+{
+  if (!buffer || bytes < 32)
+    return nullptr;
+  const uint64_t* h = (const uint64_t*)buffer;
+  if (h[0] != 0x7a6678646e69ull || bytes < 32 + h[1] * 2 + h[2] * 8)
+    return nullptr;
+  zfp_hip_index* x = new zfp_hip_index;
+  x->nblocks = h[1];
+  x->nwaves = h[2];
+  x->total_bits = h[3];
+  (void)hipGetDevice(&x->device);
+  const char* q = (const char*)buffer + 32;
+  if ((x->nblocks && hipMalloc(&x->d_len, x->nblocks * 2) != hipSuccess) ||
+      (x->nwaves && hipMalloc(&x->d_base, x->nwaves * 8) != hipSuccess)) {
+    zfp_hip_index_free(x);
+    return nullptr;
+  }
+  x->cap_blocks = x->nblocks;
+  x->cap_waves = x->nwaves;
+  if (x->nblocks)
+    (void)hipMemcpy(x->d_len, q, x->nblocks * 2, hipMemcpyHostToDevice);
+  if (x->nwaves)
+    (void)hipMemcpy(x->d_base, q + x->nblocks * 2, x->nwaves * 8, hipMemcpyHostToDevice);
+  return x;
+}
+
+int zfp_hip_last_timing(double* kernel_ms, double* total_ms)
+{
+  if (!t_last || !t_last->timed)
+    return 0;
+  if (kernel_ms) *kernel_ms = t_last->kernel_ms;
+  if (total_ms) *total_ms = t_last->total_ms;
+  return 1;
+}
+
+}  // extern "C"

@@ -1,0 +1,112 @@
+"""Chunked parallel compression of a shared array: zfp_parallel.
+
+Same surface as the reference's zfpy/_zfp_par.py (class zfp_p, :9-157):
+a shared RawArray holds the field, zfp_chunkit partitions it into chunk boxes
+(zfp_optimal_parts_from_size), compress() runs a ThreadPool over the chunks and
+keeps one self-contained stream per chunk (whole-field header + the chunk's
+blocks), decompress() writes every chunk back into the shared array.
+
+On MI355X every chunk call runs on the GPU; the worker threads overlap the
+host<->device copies and kernels of different chunks (each thread has its own
+HIP stream).  Optional `ngpus=` spreads chunk i over device i % ngpus.
+Divergences from the reference (bug fixes that do not change any output): the
+decompress hand-off does not go through a module global (:144) and the JSON
+helpers import json.  The block_size rule keeps the reference's 2^ndim.
+"""
+import json
+import math
+from multiprocessing import cpu_count
+from multiprocessing.pool import ThreadPool
+from multiprocessing.sharedctypes import RawArray
+
+import numpy as np
+
+from .zfpy_c import compress_numpy_portion, decompress_numpy_portion, device_count, zfp_chunkit
+
+_TYPECODE = {"float32": "f", "float64": "d", "int32": "i", "int64": "q"}
+_ITEMSIZE = {"float32": 4, "float64": 8, "int32": 4, "int64": 8}
+
+
+class zfp_p:
+    def __init__(self, shape, dtype, est_compression_rate=3, method="BEST_CACHE", block_size=-1, nparts=-1,
+                 ngpus=None):
+        """Args as the reference: shape, numpy dtype name, estimated compression ratio, chunking method
+        (BEST_CACHE or MAKE_EQUAL), approximate bytes per chunk (block_size) or number of parts (nparts).
+        ngpus: spread chunks over this many HIP devices (default: 1, the current device)."""
+        dtype = np.dtype(dtype).name
+        if dtype not in _TYPECODE:
+            raise ValueError(f"Unsupported NumPy dtype: {dtype}")
+        if len(shape) > 4:
+            raise ValueError("Only support up to 4 dimensions")
+        nblocks = 1
+        n123 = 1
+        for x in shape:
+            nblocks *= int((x + 3) / 4)
+            n123 *= x
+        if block_size != -1:
+            # 2^ndim (not 4^ndim) exactly as the reference (_zfp_par.py:55), so the partition matches
+            compress_block_size = math.pow(2, len(shape)) * _ITEMSIZE[dtype] / est_compression_rate
+            chunks_per_block = block_size / compress_block_size
+        elif nparts != -1:
+            chunks_per_block = nblocks / nparts
+        else:
+            raise ValueError("Either block_size or nparts must be specified")
+        self._raw_arr = RawArray(_TYPECODE[dtype], n123)
+        self._np_array = np.frombuffer(self._raw_arr, dtype=dtype).reshape(shape)
+        self._chunkit = zfp_chunkit(self._np_array, chunks_per_block, method)
+        self._compress_data = []
+        ndev = device_count()
+        self._ngpus = max(1, min(ngpus or 1, ndev if ndev > 0 else 1))
+
+    def get_raw_array(self):
+        """Return raw array representation"""
+        return self._raw_arr
+
+    def get_numpy_array(self):
+        """Return numpy array representation"""
+        return self._np_array
+
+    def get_chunkit(self):
+        return self._chunkit
+
+    def _device_of(self, ichunk):
+        return ichunk % self._ngpus if self._ngpus > 1 else -1
+
+    def compress(self, nthreads=-1, tolerance=-1, rate=-1, precision=-1):
+        """Compress every chunk; result kept in self._compress_data (list of bytes, one per chunk)."""
+        if nthreads == -1:
+            nthreads = cpu_count()
+        tasks = [(i, tolerance, rate, precision) for i in range(self._chunkit.get_nchunks())]
+
+        def one(i, tol, r, p):
+            return compress_numpy_portion(self._raw_arr, self._chunkit, i, tol, r, p, device=self._device_of(i))
+
+        with ThreadPool(processes=max(1, min(nthreads, len(tasks) or 1))) as pool:
+            self._compress_data = pool.starmap(one, tasks)
+        return self._compress_data
+
+    def decompress(self, nthreads=-1):
+        """Decompress every chunk stream into the shared array."""
+        if nthreads == -1:
+            nthreads = cpu_count()
+        data = self._compress_data
+        if len(data) != self._chunkit.get_nchunks():
+            raise RuntimeError("no compressed data for this partition (call compress first)")
+
+        def one(i):
+            decompress_numpy_portion(data[i], self._np_array, self._chunkit, i, device=self._device_of(i))
+
+        with ThreadPool(processes=max(1, min(nthreads, len(data) or 1))) as pool:
+            pool.map(one, range(len(data)))
+
+
+def write_json_header(filename, dimensions, block_splits, compressed_files):
+    """JSON sidecar: dimensions, per-axis split, compressed file name(s) (_zfp_par.py:159-175)."""
+    header = {"dimensions": dimensions, "block_splits": block_splits, "compressed_files": compressed_files}
+    with open(filename, "w") as f:
+        json.dump(header, f, indent=4)
+
+
+def read_json_header(filename):
+    with open(filename, "r") as f:
+        return json.load(f)

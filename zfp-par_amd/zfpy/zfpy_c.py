@@ -1,0 +1,517 @@
+"""zfpy_c for MI355X: the reference's Cython module surface over ctypes.
+
+Mirrors python/zfpy_c.pyx of SEP-software/zfp-par (function names, argument
+meaning, return types, error behaviour) but drives this framework's libzfp.so,
+whose zfp_compress / zfp_decompress run on the GPU.  ctypes releases the GIL
+for every foreign call, like the reference's `with nogil:` blocks (pyx:317,
+:364, :587), so a ThreadPool over chunks runs concurrently.
+
+Additions (keyword-only, optional):
+  * `device=` on the compress/decompress functions selects the HIP device;
+  * arrays exposing __cuda_array_interface__ (e.g. torch CUDA tensors) are
+    accepted by compress_numpy and compressed straight from device memory;
+  * variable-rate streams carry their GPU block index as an attribute of the
+    returned bytes object (`ZfpBytes.block_index`); decompress uses it.
+"""
+import ctypes
+import itertools
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIBPATH = os.path.join(os.path.dirname(_HERE), "lib", "libzfp.so")
+if not os.path.exists(_LIBPATH):
+    raise ImportError("zfpy: native library %s is missing (build: make -C zfp-par_amd)" % _LIBPATH)
+if os.environ.get("ZFPY_NO_TORCH") != "1":
+    # PyTorch-ROCm bundles a HIP runtime with the same SONAME as /opt/rocm's but
+    # reaches it through an unversioned NEEDED entry; if libzfp loaded first the
+    # process would map two runtimes.  Loading torch first makes both share one.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+_lib = ctypes.CDLL(_LIBPATH)
+
+_vp, _sz, _u32, _i32, _dbl, _u64, _pd = (ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint, ctypes.c_int,
+                                         ctypes.c_double, ctypes.c_uint64, ctypes.c_ssize_t)
+for _name, _res, _args in [
+    ("zfp_stream_open", _vp, [_vp]), ("zfp_stream_close", None, [_vp]),
+    ("zfp_stream_set_bit_stream", None, [_vp, _vp]), ("zfp_stream_rewind", None, [_vp]),
+    ("zfp_stream_set_rate", _dbl, [_vp, _dbl, _i32, _u32, _i32]),
+    ("zfp_stream_set_precision", _u32, [_vp, _u32]), ("zfp_stream_set_accuracy", _dbl, [_vp, _dbl]),
+    ("zfp_stream_set_reversible", None, [_vp]), ("zfp_stream_compression_mode", _i32, [_vp]),
+    ("zfp_stream_params", None, [_vp, _vp, _vp, _vp, _vp]), ("zfp_stream_rate", _dbl, [_vp, _u32]),
+    ("zfp_stream_precision", _u32, [_vp]), ("zfp_stream_accuracy", _dbl, [_vp]),
+    ("zfp_stream_maximum_size", _sz, [_vp, _vp]), ("zfp_stream_maximum_size_chunk", _sz, [_vp, _vp, _vp]),
+    ("zfp_stream_set_hip_device", _i32, [_vp, _i32]), ("zfp_stream_hip_index", _vp, [_vp]),
+    ("zfp_stream_set_hip_index", _i32, [_vp, _vp]),
+    ("zfp_field_alloc", _vp, []), ("zfp_field_1d", _vp, [_vp, _i32, _sz]),
+    ("zfp_field_2d", _vp, [_vp, _i32, _sz, _sz]), ("zfp_field_3d", _vp, [_vp, _i32, _sz, _sz, _sz]),
+    ("zfp_field_4d", _vp, [_vp, _i32, _sz, _sz, _sz, _sz]), ("zfp_field_free", None, [_vp]),
+    ("zfp_field_set_pointer", None, [_vp, _vp]), ("zfp_field_set_type", _i32, [_vp, _i32]),
+    ("zfp_field_set_stride_1d", None, [_vp, _pd]), ("zfp_field_set_stride_2d", None, [_vp, _pd, _pd]),
+    ("zfp_field_set_stride_3d", None, [_vp, _pd, _pd, _pd]),
+    ("zfp_field_set_stride_4d", None, [_vp, _pd, _pd, _pd, _pd]),
+    ("zfp_compress", _sz, [_vp, _vp]), ("zfp_decompress", _sz, [_vp, _vp]),
+    ("zfp_compress_chunk", _sz, [_vp, _vp, _vp]), ("zfp_decompress_chunk", _sz, [_vp, _vp, _vp]),
+    ("zfp_write_header", _sz, [_vp, _vp, _u32]), ("zfp_read_header", _sz, [_vp, _vp, _u32]),
+    ("zfp_optimal_parts_from_size", _vp, [_i32, _vp, ctypes.c_float, _i32]),
+    ("zfp_chunks_from_blocks", _vp, [_i32, _vp, _vp]), ("zfp_blocks_free", None, [_vp]),
+    ("zfp_chunks_free", None, [_vp]),
+    ("stream_open", _vp, [_vp, _sz]), ("stream_close", None, [_vp]),
+    ("zfp_hip_index_free", None, [_vp]), ("zfp_hip_index_export", _sz, [_vp, _vp, _sz]),
+    ("zfp_hip_index_import", _vp, [_vp, _sz]), ("zfp_hip_device_count", _i32, []),
+]:
+    _fn = getattr(_lib, _name)
+    _fn.restype = _res
+    _fn.argtypes = _args
+
+
+class _Field(ctypes.Structure):
+    """zfp_field (include/zfp.h)."""
+    _fields_ = [("type", _i32), ("nx", _sz), ("ny", _sz), ("nz", _sz), ("nw", _sz),
+                ("sx", _pd), ("sy", _pd), ("sz", _pd), ("sw", _pd), ("data", _vp)]
+
+
+class _Chunk(ctypes.Structure):
+    _fields_ = [("fx", _sz), ("fy", _sz), ("fz", _sz), ("fw", _sz),
+                ("ex", _sz), ("ey", _sz), ("ez", _sz), ("ew", _sz)]
+
+
+class _Chunks(ctypes.Structure):
+    _fields_ = [("nchunks", _sz), ("chunks", ctypes.POINTER(ctypes.POINTER(_Chunk)))]
+
+
+# exported #defines and enums (pyx:35-50)
+HEADER_MAGIC = 0x1
+HEADER_META = 0x2
+HEADER_MODE = 0x4
+HEADER_FULL = 0x7
+HEADER_MAX_BITS = 148
+
+type_none = 0
+type_int32 = 1
+type_int64 = 2
+type_float = 3
+type_double = 4
+mode_null = 0
+mode_expert = 1
+mode_fixed_rate = 2
+mode_fixed_precision = 3
+mode_fixed_accuracy = 4
+mode_reversible = 5
+
+
+def dtype_to_ztype(dtype):
+    dtype = np.dtype(dtype)
+    for dt, zt in ((np.int32, type_int32), (np.int64, type_int64), (np.float32, type_float),
+                   (np.float64, type_double)):
+        if dtype == dt:
+            return zt
+    raise TypeError("Unknown dtype: {}".format(dtype))
+
+
+def dtype_to_format(dtype):
+    dtype = np.dtype(dtype)
+    for dt, fmt in ((np.int32, "i"), (np.int64, "q"), (np.float32, "f"), (np.float64, "d")):
+        if dtype == dt:
+            return fmt
+    raise TypeError("Unknown dtype: {}".format(dtype))
+
+
+_zfp_to_dtype = {type_int32: np.int32, type_int64: np.int64, type_float: np.float32, type_double: np.float64}
+
+
+def ztype_to_dtype(ztype):
+    try:
+        return _zfp_to_dtype[ztype]
+    except KeyError:
+        raise ValueError("Unsupported zfp_type {}".format(ztype))
+
+
+_mode_names = {mode_null: "null", mode_expert: "expert", mode_reversible: "reversible",
+               mode_fixed_accuracy: "tolerance", mode_fixed_precision: "precision", mode_fixed_rate: "rate"}
+
+
+def zmode_to_str(zmode):
+    try:
+        return _mode_names[zmode]
+    except KeyError:
+        raise ValueError("Unsupported zfp_mode {}".format(zmode))
+
+
+class ZfpBytes(bytes):
+    """Compressed stream (a bytes object) that may carry its GPU block index."""
+    block_index = None
+
+
+def _check_native(ret, what):
+    if ret == 0:
+        raise RuntimeError(what)
+    return ret
+
+
+def _set_compression_mode(stream, ztype, ndim, tolerance=-1, rate=-1, precision=-1):
+    """pyx:414-429: first non-negative of tolerance, rate, precision; else reversible."""
+    if tolerance >= 0:
+        _lib.zfp_stream_set_accuracy(stream, tolerance)
+    elif rate >= 0:
+        _lib.zfp_stream_set_rate(stream, rate, ztype, ndim, 0)
+    elif precision >= 0:
+        _lib.zfp_stream_set_precision(stream, precision)
+    else:
+        _lib.zfp_stream_set_reversible(stream)
+
+
+def _one_mode(tolerance, rate, precision):
+    if sum(1 for x in (tolerance, rate, precision) if x >= 0) > 1:
+        raise ValueError("Only one of tolerance, rate, or precision can be set")
+
+
+def _make_field(pointer, ztype, shape_xfirst, strides_xfirst=None):
+    nd = len(shape_xfirst)
+    ctor = (_lib.zfp_field_1d, _lib.zfp_field_2d, _lib.zfp_field_3d, _lib.zfp_field_4d)
+    if nd < 1 or nd > 4:
+        raise RuntimeError("Greater than 4 dimensions not supported")
+    field = ctor[nd - 1](pointer, ztype, *shape_xfirst)
+    if strides_xfirst is not None:
+        setter = (_lib.zfp_field_set_stride_1d, _lib.zfp_field_set_stride_2d, _lib.zfp_field_set_stride_3d,
+                  _lib.zfp_field_set_stride_4d)
+        setter[nd - 1](field, *strides_xfirst)
+    return field
+
+
+def _export_index(stream):
+    idx = _lib.zfp_stream_hip_index(stream)
+    if not idx:
+        return None
+    need = _lib.zfp_hip_index_export(idx, None, 0)
+    buf = ctypes.create_string_buffer(need)
+    if _lib.zfp_hip_index_export(idx, buf, need) != need:
+        return None
+    return buf.raw
+
+
+def _attach_index(stream, blob):
+    if not blob:
+        return None
+    idx = _lib.zfp_hip_index_import(blob, len(blob))
+    if idx:
+        _lib.zfp_stream_set_hip_index(stream, idx)
+    return idx
+
+
+def _array_pointer(arr):
+    """(pointer, shape, strides in elements, dtype) for numpy or CUDA-array objects."""
+    cai = getattr(arr, "__cuda_array_interface__", None)
+    if cai is not None:
+        dtype = np.dtype(cai["typestr"])
+        shape = tuple(cai["shape"])
+        st = cai.get("strides")
+        if st is None:
+            st, acc = [], dtype.itemsize
+            for n in reversed(shape):
+                st.insert(0, acc)
+                acc *= n
+        return cai["data"][0], shape, [s // dtype.itemsize for s in st], dtype
+    if not isinstance(arr, np.ndarray):
+        raise TypeError("Input must be a numpy array or expose __cuda_array_interface__")
+    return arr.ctypes.data, arr.shape, [s // arr.itemsize for s in arr.strides], arr.dtype
+
+
+def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, *, device=-1):
+    """Compress a whole array into one stream (pyx:281-328)."""
+    if arr is None:
+        raise TypeError("Input array cannot be None")
+    _one_mode(tolerance, rate, precision)
+    ptr, shape, strides, dtype = _array_pointer(arr)
+    ndim = len(shape)
+    field = _make_field(ptr, dtype_to_ztype(dtype), list(reversed(shape)), list(reversed(strides)))
+    stream = _lib.zfp_stream_open(None)
+    bstream = None
+    try:
+        if device >= 0:
+            _lib.zfp_stream_set_hip_device(stream, device)
+        _set_compression_mode(stream, type_none, ndim, tolerance, rate, precision)
+        maxsize = _lib.zfp_stream_maximum_size(stream, field)
+        buf = ctypes.create_string_buffer(maxsize)
+        bstream = _lib.stream_open(buf, maxsize)
+        _lib.zfp_stream_set_bit_stream(stream, bstream)
+        _lib.zfp_stream_rewind(stream)
+        if write_header and _lib.zfp_write_header(stream, field, HEADER_FULL) == 0:
+            raise RuntimeError("Failed to write header to stream")
+        n = _lib.zfp_compress(stream, field)
+        if n == 0:
+            raise RuntimeError("Failed to write to stream")
+        out = ZfpBytes(ctypes.string_at(buf, n))
+        out.block_index = _export_index(stream)
+        return out
+    finally:
+        _lib.zfp_field_free(field)
+        _lib.zfp_stream_close(stream)
+        if bstream:
+            _lib.stream_close(bstream)
+
+
+def _decompress_into(stream, field_ptr, out, blob):
+    fld = ctypes.cast(field_ptr, ctypes.POINTER(_Field)).contents
+    fld.data = out.ctypes.data
+    idx = _attach_index(stream, blob)
+    try:
+        ret = _lib.zfp_decompress(stream, field_ptr)
+    finally:
+        if idx:
+            _lib.zfp_stream_set_hip_index(stream, None)
+            _lib.zfp_hip_index_free(idx)
+    if ret == 0:
+        raise RuntimeError("error during zfp decompression")
+    return out
+
+
+def decompress_numpy(compressed_data, *, device=-1):
+    """Decompress a stream written with a full header (pyx:533-557)."""
+    if compressed_data is None:
+        raise TypeError("compressed_data cannot be None")
+    data = bytes(compressed_data)
+    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    field = _lib.zfp_field_alloc()
+    bstream = _lib.stream_open(buf, len(data))
+    stream = _lib.zfp_stream_open(bstream)
+    try:
+        if device >= 0:
+            _lib.zfp_stream_set_hip_device(stream, device)
+        if _lib.zfp_read_header(stream, field, HEADER_FULL) == 0:
+            raise ValueError("Failed to read required zfp header")
+        fld = ctypes.cast(field, ctypes.POINTER(_Field)).contents
+        shape = tuple(n for n in (fld.nw, fld.nz, fld.ny, fld.nx) if n > 0)
+        out = np.empty(shape, dtype=ztype_to_dtype(fld.type))
+        return _decompress_into(stream, field, out, getattr(compressed_data, "block_index", None))
+    finally:
+        _lib.zfp_field_free(field)
+        _lib.zfp_stream_close(stream)
+        _lib.stream_close(bstream)
+
+
+def _decompress(compressed_data, ztype, shape, out=None, tolerance=-1, rate=-1, precision=-1, *, device=-1):
+    """Headerless decompression with caller-supplied type, shape and mode (pyx:450-531)."""
+    if compressed_data is None:
+        raise TypeError("compressed_data cannot be None")
+    if compressed_data is out:
+        raise ValueError("Cannot decompress in-place")
+    if len(shape) > 4:
+        raise ValueError("User-provided shape has too many dimensions (up to 4 supported)")
+    if len(shape) <= 0:
+        raise ValueError("User-provided shape needs at least one dimension")
+    data = bytes(compressed_data)
+    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    bstream = _lib.stream_open(buf, len(data))
+    stream = _lib.zfp_stream_open(bstream)
+    dtype = ztype_to_dtype(ztype)
+    zshape = [int(x) for x in itertools.islice(itertools.chain(reversed(shape), itertools.repeat(0)), 4)]
+    field = _lib.zfp_field_alloc()
+    try:
+        if device >= 0:
+            _lib.zfp_stream_set_hip_device(stream, device)
+        fld = ctypes.cast(field, ctypes.POINTER(_Field)).contents
+        fld.nx, fld.ny, fld.nz, fld.nw = zshape
+        _lib.zfp_field_set_type(field, ztype)
+        ndim = sum(1 for x in zshape if x > 0)
+        _set_compression_mode(stream, ztype, ndim, tolerance, rate, precision)
+        if out is None:
+            output = np.empty(tuple(x for x in shape if x > 0), dtype=dtype)
+        elif isinstance(out, np.ndarray):
+            if out.dtype != dtype:
+                raise ValueError("Out ndarray has dtype {} but decompression is using {}. Use out=ndarray.data "
+                                 "to avoid this check.".format(out.dtype, dtype))
+            if list(out.shape) != [x for x in shape if x > 0]:
+                raise ValueError("Out ndarray has shape {} but decompression is using {}.  Use out=ndarray.data "
+                                 "to avoid this check.".format(out.shape, [x for x in shape if x > 0]))
+            output = out
+        else:
+            output = np.frombuffer(out, dtype=dtype).reshape(shape)
+        return _decompress_into(stream, field, output, getattr(compressed_data, "block_index", None))
+    finally:
+        _lib.zfp_field_free(field)
+        _lib.zfp_stream_close(stream)
+        _lib.stream_close(bstream)
+
+
+def header(compressed_data):
+    """Stream header as a dict (pyx:596-650; `expert.maxbits` reports minbits as the reference does)."""
+    if compressed_data is None:
+        raise TypeError("compressed_data cannot be None")
+    data = bytes(compressed_data)
+    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    field = _lib.zfp_field_alloc()
+    bstream = _lib.stream_open(buf, len(data))
+    stream = _lib.zfp_stream_open(bstream)
+    try:
+        if _lib.zfp_read_header(stream, field, HEADER_FULL) == 0:
+            raise ValueError("Failed to read required zfp header")
+        mode = _lib.zfp_stream_compression_mode(stream)
+        fld = ctypes.cast(field, ctypes.POINTER(_Field)).contents
+        ndim = sum(1 for n in (fld.nx, fld.ny, fld.nz, fld.nw) if n > 0)
+        mb, xb, mp, me = _u32(), _u32(), _u32(), _i32()
+        _lib.zfp_stream_params(stream, ctypes.byref(mb), ctypes.byref(xb), ctypes.byref(mp), ctypes.byref(me))
+        return {
+            "nx": int(fld.nx), "ny": int(fld.ny), "nz": int(fld.nz), "nw": int(fld.nw),
+            "type": ztype_to_dtype(fld.type), "mode": zmode_to_str(mode),
+            "config": {
+                "mode": int(mode),
+                "tolerance": float(_lib.zfp_stream_accuracy(stream)),
+                "rate": float(_lib.zfp_stream_rate(stream, ndim)),
+                "precision": int(_lib.zfp_stream_precision(stream)),
+                "expert": {"minbits": int(mb.value), "maxbits": int(mb.value), "maxprec": int(mp.value),
+                           "minexp": int(me.value)},
+            },
+        }
+    finally:
+        _lib.zfp_field_free(field)
+        _lib.zfp_stream_close(stream)
+        _lib.stream_close(bstream)
+
+
+class zfp_chunkit:
+    """Chunk partition of an array (pyx:137-193): zfp_optimal_parts_from_size +
+    zfp_chunks_from_blocks with zfp axis order (x = last numpy axis)."""
+
+    def __init__(self, arr, chunks_per_block, method="BEST_CACHE"):
+        method_opts = {"BEST_CACHE": 1, "MAKE_EQUAL": 2}
+        method_c = method_opts.get(method, -1)
+        if method_c == -1:
+            raise ValueError("Invalid method '{}'. Valid options are: {}".format(method, ", ".join(method_opts)))
+        shape = tuple(getattr(arr, "shape"))
+        self.ndim = len(shape)
+        nsize = (ctypes.c_int * self.ndim)(*[int(shape[self.ndim - 1 - i]) for i in range(self.ndim)])
+        blocks = _lib.zfp_optimal_parts_from_size(self.ndim, nsize, ctypes.c_float(chunks_per_block), method_c)
+        if not blocks:
+            raise MemoryError("Failed to allocate zfp_blocks")
+        chunks = _lib.zfp_chunks_from_blocks(self.ndim, nsize, blocks)
+        if not chunks:
+            _lib.zfp_blocks_free(blocks)
+            raise MemoryError("Failed to allocate zfp_chunks")
+        cs = ctypes.cast(chunks, ctypes.POINTER(_Chunks)).contents
+        self.boxes = []
+        for i in range(cs.nchunks):
+            c = cs.chunks[i].contents
+            self.boxes.append(((c.fx, c.ex), (c.fy, c.ey), (c.fz, c.ez), (c.fw, c.ew)))
+        self.nchunks = int(cs.nchunks)
+        self._chunks = chunks
+        self._blocks = blocks
+        self.ns_python = list(shape)
+        self.n123 = int(np.prod(shape)) if shape else 0
+        self.dtype = np.dtype(getattr(arr, "dtype"))
+
+    def __del__(self):
+        try:
+            _lib.zfp_chunks_free(self._chunks)
+            _lib.zfp_blocks_free(self._blocks)
+        except Exception:
+            pass
+
+    def chunk_ptr(self, ichunk):
+        cs = ctypes.cast(self._chunks, ctypes.POINTER(_Chunks)).contents
+        if not 0 <= ichunk < cs.nchunks:
+            raise IndexError("chunk index out of range")
+        return ctypes.cast(cs.chunks[ichunk], _vp)
+
+    def get_nchunks(self):
+        return self.nchunks
+
+    def get_ndim(self):
+        return self.ndim  # (the reference's version recurses forever)
+
+    def get_dtype(self):
+        return self.dtype
+
+    def get_shape(self):
+        return self.ns_python
+
+
+def _raw_pointer(py_raw_array):
+    cai = getattr(py_raw_array, "__cuda_array_interface__", None)
+    if cai is not None:
+        return cai["data"][0]
+    if isinstance(py_raw_array, np.ndarray):
+        return py_raw_array.ctypes.data
+    return ctypes.addressof(ctypes.c_char.from_buffer(py_raw_array))
+
+
+def _init_field_raw(py_raw_array, chunkit):
+    """Field over a raw buffer: zfp order sizes, strides (1, nx, nx*ny, ...) set explicitly (pyx:196-250)."""
+    nd = chunkit.ndim
+    shape = [chunkit.ns_python[nd - 1 - i] for i in range(nd)]
+    strides = [1]
+    for i in range(nd - 1):
+        strides.append(strides[i] * shape[i])
+    return _make_field(_raw_pointer(py_raw_array), dtype_to_ztype(chunkit.dtype), shape, strides)
+
+
+def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1, precision=-1, write_header=True,
+                           *, device=-1):
+    """Compress one chunk into a self-contained stream: full whole-field header + the chunk's blocks
+    (pyx:330-376).  The buffer reserves header room (the reference under-allocates)."""
+    if py_raw_array is None:
+        raise TypeError("Input array cannot be None")
+    _one_mode(tolerance, rate, precision)
+    field = _init_field_raw(py_raw_array, chunkit)
+    stream = _lib.zfp_stream_open(None)
+    bstream = None
+    try:
+        if device >= 0:
+            _lib.zfp_stream_set_hip_device(stream, device)
+        _set_compression_mode(stream, type_none, chunkit.ndim, tolerance, rate, precision)
+        ck = chunkit.chunk_ptr(ichunk)
+        maxsize = _lib.zfp_stream_maximum_size_chunk(stream, field, ck) + (HEADER_MAX_BITS + 63) // 64 * 8 + 8
+        buf = ctypes.create_string_buffer(maxsize)
+        bstream = _lib.stream_open(buf, maxsize)
+        _lib.zfp_stream_set_bit_stream(stream, bstream)
+        _lib.zfp_stream_rewind(stream)
+        if write_header and _lib.zfp_write_header(stream, field, HEADER_FULL) == 0:
+            raise RuntimeError("Failed to write header to stream")
+        n = _lib.zfp_compress_chunk(stream, ck, field)
+        if n == 0:
+            raise RuntimeError("Failed to write to stream")
+        out = ZfpBytes(ctypes.string_at(buf, n))
+        out.block_index = _export_index(stream)
+        return out
+    finally:
+        _lib.zfp_field_free(field)
+        _lib.zfp_stream_close(stream)
+        if bstream:
+            _lib.stream_close(bstream)
+
+
+def decompress_numpy_portion(compressed_data, py_raw_array, chunkit, ichunk, *, device=-1):
+    """Decompress one chunk stream into its box of the shared array (pyx:559-593).  Like the
+    reference, zfp_read_header resets the field strides to contiguous and nothing is returned."""
+    if compressed_data is None:
+        raise TypeError("compressed_data cannot be None")
+    field = _init_field_raw(py_raw_array, chunkit)
+    data = bytes(compressed_data)
+    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    bstream = _lib.stream_open(buf, len(data))
+    stream = _lib.zfp_stream_open(bstream)
+    idx = None
+    try:
+        if device >= 0:
+            _lib.zfp_stream_set_hip_device(stream, device)
+        if _lib.zfp_read_header(stream, field, HEADER_FULL) == 0:
+            raise ValueError("Failed to read required zfp header")
+        idx = _attach_index(stream, getattr(compressed_data, "block_index", None))
+        ret = _lib.zfp_decompress_chunk(stream, chunkit.chunk_ptr(ichunk), field)
+        if ret == 0:
+            raise RuntimeError("error during zfp decompression")
+    finally:
+        if idx:
+            _lib.zfp_stream_set_hip_index(stream, None)
+            _lib.zfp_hip_index_free(idx)
+        _lib.zfp_field_free(field)
+        _lib.zfp_stream_close(stream)
+        _lib.stream_close(bstream)
+
+
+def device_count():
+    """Number of visible HIP devices."""
+    return int(_lib.zfp_hip_device_count())

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Light driver for profiling: device-resident zfp_compress / zfp_decompress loops.
+
+usage: python tools/kprof.py [--mode rate|precision|reversible] [--param P] [--dtype f32|f64]
+                             [--n 1024] [--iters 5] [--decode]
+Prints per-call kernel ms from the library's HIP events.
+"""
+import argparse
+import ctypes
+import os
+import sys
+import time
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [R, R + "/tests", R + "/oracle"]
+
+
+def field(torch, n, dtype, dev):
+    x = torch.arange(n, device=dev, dtype=torch.float64)
+    out = torch.empty((n, n, n), device=dev, dtype=dtype)
+    base = torch.sin(0.05 * x)[None, :] * torch.cos(0.03 * x)[:, None]
+    xy = 0.01 * x[None, :] * x[:, None] / n
+    for z0 in range(0, n, 64):
+        z = torch.arange(z0, min(n, z0 + 64), device=dev, dtype=torch.float64)[:, None, None]
+        out[z0:z0 + 64] = (base[None] + 0.5 * torch.sin(0.02 * z + xy[None])).to(dtype)
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="rate")
+    ap.add_argument("--param", type=float, default=16)
+    ap.add_argument("--dtype", default="f32")
+    ap.add_argument("--n", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--decode", action="store_true")
+    a = ap.parse_args()
+    import torch
+    from capi import ZfpCAPI
+    api = ZfpCAPI(R + "/zfp-par_amd/lib/libzfp.so")
+    api.enable_index()
+    lib = api.lib
+    dev = torch.device("cuda", 0)
+    dt = torch.float32 if a.dtype == "f32" else torch.float64
+    zt = 3 if a.dtype == "f32" else 4
+    f = field(torch, a.n, dt, dev)
+    zf = lib.zfp_field_3d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.n)
+    zs = lib.zfp_stream_open(None)
+    api.set_mode(zs, a.mode, a.param if a.mode != "reversible" else None, zt, 3)
+    cap = lib.zfp_stream_maximum_size(zs, zf)
+    out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+    bs = lib.stream_open(ctypes.c_void_p(out.data_ptr()), cap)
+    lib.zfp_stream_set_bit_stream(zs, bs)
+    ks = []
+    for i in range(a.iters):
+        lib.zfp_stream_rewind(zs)
+        nb = lib.zfp_compress(zs, zf)
+        assert nb, lib.zfp_hip_last_error()
+        k, t = ctypes.c_double(), ctypes.c_double()
+        lib.zfp_hip_last_timing(ctypes.byref(k), ctypes.byref(t))
+        ks.append(k.value)
+    gb = f.numel() * f.element_size() / 1e9
+    print("encode %s %s %s: bytes=%d kernel_ms=%s  GB/s=%.1f" % (a.dtype, a.mode, a.param, nb,
+          " ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
+    if a.decode:
+        back = torch.empty_like(f)
+        lib.zfp_field_set_pointer(zf, ctypes.c_void_p(back.data_ptr()))
+        ks = []
+        for i in range(a.iters):
+            lib.stream_rewind(bs)
+            assert lib.zfp_decompress(zs, zf), lib.zfp_hip_last_error()
+            k, t = ctypes.c_double(), ctypes.c_double()
+            lib.zfp_hip_last_timing(ctypes.byref(k), ctypes.byref(t))
+            ks.append(k.value)
+        print("decode kernel_ms=%s  GB/s=%.1f" % (" ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
+
+
+if __name__ == "__main__":
+    main()

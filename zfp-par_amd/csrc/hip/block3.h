@@ -156,23 +156,22 @@ __device__ __forceinline__ void scatter3(const S (&v)[64], S* __restrict__ base,
 }
 
 // ---- coefficient order + negabinary, then bit planes ----
-__device__ __forceinline__ void planes_from_coeffs(uint64_t (&P)[32], const int32_t (&q)[64])
+// Planes as two 32-bit halves: Pl[k] bit i = plane k of coefficient i (i < 32),
+// Ph[k] bit i = plane k of coefficient 32 + i.
+__device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[32], uint32_t (&Ph)[32], const int32_t (&q)[64])
 {
-  uint32_t lo[32], hi[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    lo[i] = ((uint32_t)q[kPerm3[i]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
-    hi[i] = ((uint32_t)q[kPerm3[i + 32]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    Pl[i] = ((uint32_t)q[kPerm3[i]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    Ph[i] = ((uint32_t)q[kPerm3[i + 32]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
   }
-  transpose32(lo);
-  transpose32(hi);
-#pragma unroll
-  for (int k = 0; k < 32; k++)
-    P[k] = (uint64_t)lo[k] | ((uint64_t)hi[k] << 32);
+  transpose32(Pl);
+  transpose32(Ph);
 }
 
 // double: planes 32..63 from the high words; 0..31 only when `need_low`
-__device__ __forceinline__ void planes_from_coeffs(uint64_t (&P)[64], const int64_t (&q)[64], bool need_low)
+__device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[64], uint32_t (&Ph)[64], const int64_t (&q)[64],
+                                                   bool need_low)
 {
   uint32_t a[32], b[32];
 #pragma unroll
@@ -185,8 +184,10 @@ __device__ __forceinline__ void planes_from_coeffs(uint64_t (&P)[64], const int6
   transpose32(a);
   transpose32(b);
 #pragma unroll
-  for (int k = 0; k < 32; k++)
-    P[32 + k] = (uint64_t)a[k] | ((uint64_t)b[k] << 32);
+  for (int k = 0; k < 32; k++) {
+    Pl[32 + k] = a[k];
+    Ph[32 + k] = b[k];
+  }
   if (__any(need_low)) {
 #pragma unroll
     for (int i = 0; i < 32; i++) {
@@ -198,12 +199,16 @@ __device__ __forceinline__ void planes_from_coeffs(uint64_t (&P)[64], const int6
     transpose32(a);
     transpose32(b);
 #pragma unroll
-    for (int k = 0; k < 32; k++)
-      P[k] = (uint64_t)a[k] | ((uint64_t)b[k] << 32);
+    for (int k = 0; k < 32; k++) {
+      Pl[k] = a[k];
+      Ph[k] = b[k];
+    }
   } else {
 #pragma unroll
-    for (int k = 0; k < 32; k++)
-      P[k] = 0;
+    for (int k = 0; k < 32; k++) {
+      Pl[k] = 0;
+      Ph[k] = 0;
+    }
   }
 }
 
@@ -265,18 +270,20 @@ __device__ __forceinline__ uint32_t precision3(int emax, const CodecParams& cp)
   return (uint32_t)p < cp.maxprec ? (uint32_t)p : cp.maxprec;
 }
 
-// integer part of the block: order, planes, coder (encode.c:260-280)
+// integer part of the block: order, planes, coder (encode.c:260-280).
+// Codes from bit `pos` of the slot; returns the end position (<= lim).
 template <typename Int>
-__device__ __forceinline__ uint32_t encode_ints3(SlotWriter& w, Int (&q)[64], uint32_t budget, uint32_t prec)
+__device__ __forceinline__ uint32_t encode_ints3(OrSlot& w, const uint32_t* lut, Int (&q)[64], uint32_t pos,
+                                                 uint32_t lim, uint32_t prec)
 {
   using S = typename std::conditional<sizeof(Int) == 4, float, double>::type;
   constexpr int PREC = Traits<S>::kIntPrec;
-  uint64_t P[PREC];
+  uint32_t Pl[PREC], Ph[PREC];
   if constexpr (PREC == 32)
-    planes_from_coeffs(P, q);
+    planes_from_coeffs(Pl, Ph, q);
   else
-    planes_from_coeffs(P, q, prec > 32);
-  return code_planes64<PREC>(w, budget, prec, P);
+    planes_from_coeffs(Pl, Ph, q, prec > 32);
+  return code_planes<PREC>(w, lut, pos, lim, prec, Pl, Ph);
 }
 
 template <typename Int>
@@ -293,10 +300,55 @@ __device__ __forceinline__ uint32_t decode_ints3(WordReader& r, Int (&q)[64], ui
   return used;
 }
 
-// Encode one block; returns its length in bits including minbits padding
-// (padding bits are zeros and are NOT written to the slot).
+// Block exponent and block-floating-point cast for the lossy encoder.  Fast
+// path: the max magnitude comes from integer maxima of the bit patterns (NaN
+// sorts above inf, so one compare flags inf/NaN blocks), and for a finite
+// block with a finite scale s*x < 2^30 always, so the hardware conversion
+// matches C's.  Blocks holding inf/NaN or with a scale that overflows take the
+// exact path (NaN-ignoring max, x86 INT_MIN conversions); the branch is
+// uniform and skipped unless some lane in the wave needs it.
+__device__ __forceinline__ int lossy_emax_cast(int32_t (&q)[64], const float (&v)[64], const CodecParams& cp,
+                                               uint32_t& mp)
+{
+  int32_t mi = 0;
+  uint32_t mu = 0;
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    const uint32_t b = __float_as_uint(v[i]);
+    mi = max(mi, (int32_t)b);
+    mu = max(mu, b);
+  }
+  const uint32_t mb = max((uint32_t)mi, mu & 0x7fffffffu);
+  int emax = mb == 0 ? -127 : ((mb >> 23) == 0 ? -126 : (int)(mb >> 23) - 126);
+  const bool bad = mb >= 0x7f800000u;
+  if (bad)
+    emax = block_emax(block_absmax(v));
+  mp = precision3(emax, cp);
+  const bool cast = mp != 0 && emax != -127;
+  if (__any(cast && (bad || emax < -97))) {
+    fwd_cast(q, v, emax);
+  } else {
+    const float s = __uint_as_float((uint32_t)(157 - emax) << 23);
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      q[i] = (int32_t)(s * v[i]);
+  }
+  return emax;
+}
+
+__device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], const double (&v)[64], const CodecParams& cp,
+                                               uint32_t& mp)
+{
+  const int emax = block_emax(block_absmax(v));
+  mp = precision3(emax, cp);
+  fwd_cast(q, v, emax);
+  return emax;
+}
+
+// Encode one block into a zeroed slot; returns its length in bits including
+// minbits padding (padding bits are the slot's zeros).
 template <typename S, bool REV>
-__device__ __forceinline__ uint32_t encode_block3(SlotWriter& w, S (&v)[64], const CodecParams& cp)
+__device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut, S (&v)[64], const CodecParams& cp)
 {
   using T = Traits<S>;
   using Int = typename T::Int;
@@ -324,11 +376,10 @@ __device__ __forceinline__ uint32_t encode_block3(SlotWriter& w, S (&v)[64], con
     if (same) {
       uint32_t e = (uint32_t)(emax + T::kEbias);
       if (!e) {
-        w.put(0, 1);
-        return 1;
+        // a single 0 bit (already zero in the slot)
+        return 1u < cp.minbits ? cp.minbits : 1u;
       }
-      w.put(1, 2);
-      w.put(e, kE);
+      w.put(0, 1u | ((uint64_t)e << 2), 2 + kE);
       bits = 2 + kE;
     } else {
 #pragma unroll
@@ -336,12 +387,11 @@ __device__ __forceinline__ uint32_t encode_block3(SlotWriter& w, S (&v)[64], con
         Int x = (Int)bits_of(v[i]);
         q[i] = x < 0 ? (Int)((UInt)x ^ T::kTcMask) : x;
       }
-      w.put(3, 2);
+      w.put(0, 3, 2);
       bits = 2;
     }
     // rev_encode_block_<Int> (revencode.c:54-76)
-    uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
-    uint32_t maxb = cp.maxbits - bits;
+    const uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
     xform<3, false, true>(q);
     UInt all = 0;
 #pragma unroll
@@ -352,30 +402,29 @@ __device__ __forceinline__ uint32_t encode_block3(SlotWriter& w, S (&v)[64], con
                         : 0u;
     if (prec > cp.maxprec) prec = cp.maxprec;
     if (prec < 1) prec = 1;
-    w.put(prec - 1, T::kPbits);
-    uint32_t ib = T::kPbits + encode_ints3(w, q, maxb - T::kPbits, prec);
+    w.put(bits, prec - 1, T::kPbits);
+    const uint32_t end = encode_ints3(w, lut, q, bits + T::kPbits, cp.maxbits, prec);
+    uint32_t ib = end - bits;
     if (ib < minb) ib = minb;
     return bits + ib;
   } else {
-  // lossy (encodef.c:63-90)
-  uint32_t bits = 1;
-  int emax = block_emax(block_absmax(v));
-  uint32_t mp = precision3(emax, cp);
-  uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
-  if (e) {
-    w.put(2 * (uint64_t)e + 1, 1 + kE);
-    bits += kE;
-    fwd_cast(q, v, emax);
-    xform<3, false, false>(q);
-    uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
-    uint32_t ib = encode_ints3(w, q, cp.maxbits - bits, mp);
-    if (ib < minb) ib = minb;
-    bits += ib;
-  } else {
-    w.put(0, 1);
-    if (cp.minbits > bits) bits = cp.minbits;
-  }
-  return bits;
+    // lossy (encodef.c:63-90)
+    uint32_t mp;
+    const int emax = lossy_emax_cast(q, v, cp, mp);
+    const uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
+    uint32_t bits = 1;
+    if (e) {
+      w.put(0, 2 * (uint64_t)e + 1, 1 + kE);
+      bits += kE;
+      xform<3, false, false>(q);
+      const uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
+      uint32_t ib = encode_ints3(w, lut, q, bits, cp.maxbits, mp) - bits;
+      if (ib < minb) ib = minb;
+      bits += ib;
+    } else if (cp.minbits > bits) {
+      bits = cp.minbits;
+    }
+    return bits;
   }
 }
 

@@ -66,45 +66,69 @@ __device__ __forceinline__ uint32_t ctz64(uint64_t x)
 }
 
 // ---------------------------------------------------------------------------
-// Bit writer into a lane's LDS slot (bitstream.inl:289-313 semantics:
-// values appended least-significant bit first, 64-bit little-endian words).
+// Encoder output: a per-lane slot of 64-bit words in LDS, zeroed before the
+// block is coded.  Bits are ORed in at their absolute position (LSB first,
+// bitstream.inl:289-313 word layout), so no write depends on an earlier one
+// and the coder needs no serial accumulator.  Positions past the block's
+// budget are garbage by construction: every word index is clamped to a trash
+// word (`trash`) that is never read, and readers mask at the block length.
 // ---------------------------------------------------------------------------
-struct SlotWriter {
-  uint64_t* slot;
-  uint64_t acc;
-  uint32_t fill;
-  uint32_t widx;
+__device__ __forceinline__ void lds_or(uint64_t* p, uint64_t v)
+{
+  __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
 
-  __device__ __forceinline__ void init(uint64_t* s)
+struct OrSlot {
+  uint64_t* w;
+  uint32_t trash;
+
+  __device__ __forceinline__ void or_word(uint32_t i, uint64_t v) { lds_or(w + (i < trash ? i : trash), v); }
+  // v < 2^len, len <= 64
+  __device__ __forceinline__ void put(uint32_t p, uint64_t v, uint32_t len)
   {
-    slot = s;
-    acc = 0;
-    fill = 0;
-    widx = 0;
+    const uint32_t i = p >> 6, sh = p & 63;
+    or_word(i, v << sh);
+    if (__any(sh + len > 64))
+      or_word(i + 1, (v >> 1) >> (63 - sh));
   }
-  // v must have no bits at or above n; 0 <= n <= 64
-  __device__ __forceinline__ void put(uint64_t v, uint32_t n)
+  // (lo | hi << 64) < 2^len, len <= 128.  The spill words are written under
+  // wave-uniform tests (a lane with nothing to spill ORs a zero).
+  __device__ __forceinline__ void put128(uint32_t p, uint64_t lo, uint64_t hi, uint32_t len)
   {
-    acc |= v << fill;
-    uint32_t t = fill + n;
-    if (t >= 64) {
-      slot[widx++] = acc;
-      acc = fill ? (v >> (64 - fill)) : 0ull;
-      t -= 64;
-    }
-    fill = t;
-  }
-  __device__ __forceinline__ uint32_t written() const { return widx * 64 + fill; }
-  // flush the pending partial word (zero padded)
-  __device__ __forceinline__ void finish()
-  {
-    if (fill) {
-      slot[widx++] = acc;
-      acc = 0;
-      fill = 0;
-    }
+    const uint32_t i = p >> 6, sh = p & 63;
+    or_word(i, lo << sh);
+    if (__any(sh + len > 64))
+      or_word(i + 1, ((lo >> 1) >> (63 - sh)) | (hi << sh));
+    if (__any(sh + len > 128))
+      or_word(i + 2, (hi >> 1) >> (63 - sh));
   }
 };
+
+// Doubled-ones table: entry b holds the 8 bits of b LSB first with every one
+// written twice ("1" -> "11", "0" -> "0"), 8 + popcount(b) bits.  The group
+// tests of a bit plane are this expansion of the plane's remaining bits (see
+// code_plane), so one table look-up replaces a loop over the ones.
+__device__ __forceinline__ uint32_t dbl_entry(uint32_t b)
+{
+  uint32_t d = 0, p = 0;
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    if ((b >> i) & 1u) {
+      d |= 3u << p;
+      p += 2;
+    } else {
+      p += 1;
+    }
+  }
+  return d;
+}
+
+// expansion of a 16-bit unit: 16 + popcount(u) bits
+__device__ __forceinline__ uint32_t dbl16(const uint32_t* lut, uint32_t u)
+{
+  const uint32_t b0 = u & 0xffu, b1 = (u >> 8) & 0xffu;
+  return lut[b0] | (lut[b1] << (8u + (uint32_t)__popc(b0)));
+}
 
 // Bit reader over a word array in LDS (or global memory).
 struct WordReader {
@@ -342,18 +366,27 @@ __device__ __forceinline__ void xform(Int (&p)[1 << (2 * D)])
 // Bit-matrix transpose of 32x32 bits held in 32 registers: a[r] bit c <-> a[c] bit r.
 // Used both ways: coefficients -> bit planes (encode) and back (decode).
 // ---------------------------------------------------------------------------
+// Byte-granular steps are one v_perm_b32 per output word, the rest one shift
+// plus one v_bfi_b32.
 template <int J>
 __device__ __forceinline__ void transpose_step(uint32_t (&a)[32])
 {
-  constexpr uint32_t M = (J == 16) ? 0x0000ffffu : (J == 8) ? 0x00ff00ffu : (J == 4) ? 0x0f0f0f0fu
-                                                 : (J == 2) ? 0x33333333u : 0x55555555u;
+  constexpr uint32_t M = (J == 4) ? 0x0f0f0f0fu : (J == 2) ? 0x33333333u : 0x55555555u;
 #pragma unroll
   for (int k = 0; k < 32; k++) {
     if (k & J)
       continue;
-    uint32_t t = ((a[k] >> J) ^ a[k | J]) & M;
-    a[k] ^= t << J;
-    a[k | J] ^= t;
+    const uint32_t x = a[k], y = a[k | J];
+    if constexpr (J == 16) {
+      a[k] = __builtin_amdgcn_perm(y, x, 0x05040100u);
+      a[k | J] = __builtin_amdgcn_perm(y, x, 0x07060302u);
+    } else if constexpr (J == 8) {
+      a[k] = __builtin_amdgcn_perm(y, x, 0x06020400u);
+      a[k | J] = __builtin_amdgcn_perm(y, x, 0x07030501u);
+    } else {
+      a[k] = (x & M) | ((y << J) & ~M);
+      a[k | J] = ((x >> J) & M) | (y & ~M);
+    }
   }
 }
 
@@ -375,71 +408,77 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32])
 // coefficient's closing 1 implicit), "0" ends the plane.  The budget may cut a
 // run anywhere: exactly the reference's bit-by-bit truncation.
 // ---------------------------------------------------------------------------
-// one plane of the coder (k is the plane number; P[k] its 64 bits)
-__device__ __forceinline__ void code_plane64(SlotWriter& w, uint64_t plane, uint32_t& bits, uint32_t& n)
+//
+// Closed form of one plane.  With n significant coefficients, x = plane >> n
+// (the not-yet-significant bits), h its highest one and c its popcount, the
+// reference's group tests emit "1", then for every bit of x up to h the bit
+// itself plus, after a one, the next group test's "1" -- i.e. "1" followed by
+// the doubled-ones expansion of x[0..h] with its final bit dropped -- then a
+// "0" test if n + h + 1 < 64 (otherwise the last one is implicit).  Clearing
+// the top one (x') makes the expansion garbage-free: "1" + dbl(x') is exact for
+// h + c bits and the final "1 0" (or nothing) is added as a tail.  A plane is
+// then one OR of (verbatim | group << n) into the slot plus, for lanes whose
+// x reaches past bit 15, one OR per further 16-bit unit.  The budget is not
+// checked inside a plane: bits beyond it fall past the block end.
+__device__ __forceinline__ void code_plane(OrSlot& s, const uint32_t* lut, uint64_t plane, uint32_t& n, uint32_t& pos)
 {
-  uint32_t m = n < bits ? n : bits;
-  w.put(plane & low_mask(m), m);
-  bits -= m;
-  uint64_t x = n >= 64 ? 0ull : (plane >> n);
-  while (bits && n < 64) {
-    if (!x) {
-      w.put(0, 1);
-      bits--;
-      break;
+  const bool part = n < 64;
+  const uint32_t nn = n & 63u;
+  const uint64_t x = part ? plane >> nn : 0ull;
+  const uint64_t verb = plane ^ (x << nn);
+  const bool nz = x != 0;
+  const uint32_t h = 63u - (uint32_t)__clzll((long long)(x | 1ull));
+  const uint32_t c = (uint32_t)__popcll(x);
+  const uint64_t xp = x & ~(1ull << h);
+  const bool impl = nz && (n + h == 63u);
+  const bool normal = nz && !impl;
+  const uint32_t lr = nz ? h + c : 0u;
+  const uint32_t u0 = (uint32_t)xp & 0xffffu;
+  uint64_t grp = ((uint64_t)dbl16(lut, u0) << 1) | (nz ? 1ull : 0ull);
+  if (normal && lr < 64)
+    grp |= 1ull << lr;
+  const uint32_t glen = nz ? (impl ? lr : lr + 2u) : (part ? 1u : 0u);
+  const uint64_t lo = verb | (grp << nn);
+  const uint64_t hi = nn ? (grp >> (64 - nn)) : 0ull;
+  s.put128(pos, lo, hi, n + glen);
+  if (__any(nz && h >= 16)) {
+    const uint32_t ps = pos + n;
+    uint32_t off = 17u + (uint32_t)__popc(u0);
+#pragma unroll
+    for (int j = 1; j < 4; j++) {
+      const uint32_t u = (uint32_t)(xp >> (16 * j)) & 0xffffu;
+      if (__any(u != 0))
+        s.put(ps + off, dbl16(lut, u), 32);  // u == 0 ORs zeros
+      off += 16u + (uint32_t)__popc(u);
     }
-    uint32_t t = ctz64(x);
-    uint64_t pat;
-    uint32_t len, nn;
-    if (n + t < 63) {
-      pat = 1ull | (1ull << (t + 1));
-      len = t + 2;
-      nn = n + t + 1;
-    } else {
-      pat = 1ull;
-      len = t + 1;
-      nn = 64;
-    }
-    if (len > bits) {
-      len = bits;
-      pat &= low_mask(len);
-    }
-    w.put(pat, len);
-    bits -= len;
-    x = nn >= 64 ? 0ull : (x >> (t + 1));
-    n = nn;
+    if (__any(normal && lr >= 64))
+      s.put(ps + lr, (normal && lr >= 64) ? 1ull : 0ull, 1);
   }
+  pos += n + glen;
+  n = nz ? (impl ? 64u : n + h + 1u) : n;
 }
 
-// compile-time walk over planes K, K-1, ..., 0 so that P[K] is a register
-template <int K, int PREC>
-struct EncodePlanes {
-  static __device__ __forceinline__ void run(SlotWriter& w, const uint64_t (&P)[PREC], uint32_t kmin, uint32_t& bits,
-                                             uint32_t& n)
-  {
-    bool act = bits != 0 && (uint32_t)K >= kmin;
-    if (!__any(act))
-      return;
-    if (act)
-      code_plane64(w, P[K], bits, n);
-    EncodePlanes<K - 1, PREC>::run(w, P, kmin, bits, n);
-  }
-};
-
+// Codes planes PREC-1 .. PREC-maxprec starting at bit `pos` of the slot;
+// returns the end position clamped to `lim` (the block's bit budget end).
+// The plane index is wave-uniform, so Pl[k]/Ph[k] are register reads with a
+// scalar index (no unrolling: one copy of the plane code).
 template <int PREC>
-struct EncodePlanes<-1, PREC> {
-  static __device__ __forceinline__ void run(SlotWriter&, const uint64_t (&)[PREC], uint32_t, uint32_t&, uint32_t&) {}
-};
-
-template <int PREC>
-__device__ __forceinline__ uint32_t code_planes64(SlotWriter& w, uint32_t budget, uint32_t maxprec,
-                                                  const uint64_t (&P)[PREC])
+__device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, uint32_t pos, uint32_t lim,
+                                                uint32_t maxprec, const uint32_t (&Pl)[PREC],
+                                                const uint32_t (&Ph)[PREC])
 {
   const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
-  uint32_t bits = budget;
   uint32_t n = 0;
-  EncodePlanes<PREC - 1, PREC>::run(w, P, kmin, bits, n);
-  return budget - bits;
+  for (int k = PREC - 1; k >= 0; k--) {
+    const bool act = pos < lim && (uint32_t)k >= kmin;
+    if (!__any(act))
+      break;
+    const int ku = __builtin_amdgcn_readfirstlane(k);
+    const uint64_t plane = ((uint64_t)Ph[ku] << 32) | Pl[ku];
+    if (act)
+      code_plane(s, lut, plane, n, pos);
+  }
+  return pos < lim ? pos : lim;
 }
 
 // Decoder twin (decode.c:69-246), including the reference quirk that a

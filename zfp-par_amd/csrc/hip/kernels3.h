@@ -18,6 +18,7 @@
 namespace zfp_amd {
 
 constexpr int kWavesPerGroup = 4;
+constexpr size_t kLutBytes = 256 * sizeof(uint32_t);  // static LDS of the encoders
 constexpr uint64_t kNoWord = ~0ull;
 
 struct Partial {
@@ -37,61 +38,89 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
   return x;
 }
 
+// Kernel prologue shared by the encoders: the doubled-ones table (one entry
+// per thread of the 256-thread group) and the wave's zeroed slot region.
+__device__ __forceinline__ void encode_prologue(uint32_t* lut, uint64_t* wslot, uint32_t words)
+{
+  lut[threadIdx.x] = dbl_entry(threadIdx.x);
+  const int lane = threadIdx.x & 63;
+  uint4* z = reinterpret_cast<uint4*>(wslot);
+  for (uint32_t i = lane; i < words / 2; i += 64)
+    z[i] = make_uint4(0, 0, 0, 0);
+  if ((words & 1) && lane == 0)
+    wslot[words - 1] = 0;
+  __syncthreads();
+}
+
+// floor(i / d) for i < 2^20, d < 2^12 with m = ceil(2^32 / d) (m = 0 for d = 1)
+__device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m ? __umulhi(i, m) : i; }
+
 // ---------------------------------------------------------------------------
-// Fixed rate, block size a multiple of 64 bits.  The wave's 64 blocks form one
-// contiguous run of words; with a stream offset r0 = g0 (mod 64) != 0 every
-// output word is a funnel shift of two run words, and the run's first and
-// last words (shared with neighbouring waves) go to the fix-up kernels.
+// Fixed rate, block size a multiple of 64 bits (sw words).  The wave's 64
+// blocks form one contiguous run of words; with a stream offset r0 = g0
+// (mod 64) != 0 every output word is a funnel shift of two run words, and the
+// run's first and last words (shared with neighbouring waves) go to the
+// fix-up kernels.  Slots are swp >= sw + 1 words; word sw is the trash word.
 template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        uint64_t* __restrict__ out, uint32_t sw, uint32_t swp,
-                                                       uint32_t r0, Partial* __restrict__ partials)
+                                                       uint32_t magic, uint32_t r0, Partial* __restrict__ partials)
 {
+  __shared__ uint32_t lut[256];
   extern __shared__ uint64_t lds[];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   uint64_t* wslot = lds + (size_t)wv * 64 * swp;
+  encode_prologue(lut, wslot, 64 * swp);
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
-  SlotWriter wr;
-  wr.init(wslot + (size_t)lane * swp);
   if (b < g.nblocks) {
     S v[64];
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
-    encode_block3<S, REV>(wr, v, cp);
-    wr.finish();
-    while (wr.widx < sw)
-      wr.slot[wr.widx++] = 0;
+    OrSlot os{wslot + (size_t)lane * swp, sw};
+    encode_block3<S, REV>(os, lut, v, cp);
   }
-  __syncthreads();
   if (first >= g.nblocks)
     return;
+  // slots are read across lanes of this wave only: LDS ops of a wave complete in order
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   const uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
   const uint32_t total = (uint32_t)nb * sw;  // run length in words
+  uint64_t* dst = out + first * sw;
   if (r0 == 0) {
-    uint64_t* dst = out + first * sw;
-    for (uint32_t i = lane; i < total; i += 64) {
-      uint32_t l = i / sw;
-      uint32_t k = i - l * sw;
-      dst[i] = wslot[(size_t)l * swp + k];
+    if ((sw & 1) == 0) {
+      // 16-byte stores: word pairs never straddle two slots
+      for (uint32_t i = 2 * lane; i < total; i += 128) {
+        const uint32_t l = div_magic(i, magic);
+        const uint64_t* src = wslot + (size_t)l * swp + (i - l * sw);
+        ulonglong2 q;
+        q.x = src[0];
+        q.y = src[1];
+        *reinterpret_cast<ulonglong2*>(dst + i) = q;
+      }
+    } else {
+      for (uint32_t i = lane; i < total; i += 64) {
+        const uint32_t l = div_magic(i, magic);
+        dst[i] = wslot[(size_t)l * swp + (i - l * sw)];
+      }
     }
     return;
   }
   // run words j = 0..total-1 land at bit r0 + 64 j of out[first*sw ...]
-  uint64_t* dst = out + first * sw;
   for (uint32_t j = lane; j <= total; j += 64) {
     uint64_t cur = 0, prev = 0;
     if (j < total) {
-      uint32_t l = j / sw;
+      const uint32_t l = div_magic(j, magic);
       cur = wslot[(size_t)l * swp + (j - l * sw)];
     }
     if (j > 0) {
-      uint32_t l = (j - 1) / sw;
+      const uint32_t l = div_magic(j - 1, magic);
       prev = wslot[(size_t)l * swp + (j - 1 - l * sw)];
     }
-    uint64_t val = (cur << r0) | (prev >> (64 - r0));
+    const uint64_t val = (cur << r0) | (prev >> (64 - r0));
     if (j == 0) {
       partials[2 * w] = Partial{first * sw, val};
     } else if (j == total) {
@@ -172,6 +201,7 @@ template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        GeneralArgs a)
 {
+  __shared__ uint32_t lut[256];
   extern __shared__ uint64_t lds[];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
@@ -179,6 +209,7 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   uint64_t* wbase = lds + (size_t)wv * (64 * a.swp + 64);
   uint32_t* off = reinterpret_cast<uint32_t*>(wbase + 64 * a.swp);
   uint32_t* wrt = off + 64;
+  encode_prologue(lut, wbase, 64 * a.swp);
 
   const uint64_t nwaves = (g.nblocks + 63) / 64;
   uint64_t w;
@@ -194,21 +225,19 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
 
-  SlotWriter wr;
-  wr.init(wbase + (size_t)lane * a.swp);
   uint32_t len = 0;
   if (live && b < g.nblocks) {
     S v[64];
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
-    len = encode_block3<S, REV>(wr, v, cp);
-    wr.finish();
+    OrSlot os{wbase + (size_t)lane * a.swp, a.swp - 1};
+    len = encode_block3<S, REV>(os, lut, v, cp);
   }
   const uint32_t incl = wave_incl_scan(len);
   const uint32_t excl_l = incl - len;
   const uint32_t total = __shfl(incl, 63, 64);
   off[lane] = excl_l;
-  wrt[lane] = b < g.nblocks ? (wr.widx * 64 < len ? wr.widx * 64 : len) : 0;
+  wrt[lane] = len < 64 * (a.swp - 1) ? len : 64 * (a.swp - 1);  // beyond: padding zeros
 
   uint64_t start = 0;  // bit offset of the wave's first block relative to g0
   if (!live) {

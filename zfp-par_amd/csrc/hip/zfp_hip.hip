@@ -221,9 +221,10 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   dim3 grid((unsigned)ngroups), block(256);
   if (p.fixed && (p.cp.maxbits % 64) == 0) {
     const uint32_t sw = p.cp.maxbits / 64;
-    const uint32_t swp = sw | 1;
+    const uint32_t swp = (sw + 1) | 1;  // odd stride, word sw is the trash word
+    const uint32_t magic = sw > 1 ? (uint32_t)((0x100000000ull + sw - 1) / sw) : 0u;
     size_t lds = (size_t)kWavesPerGroup * 64 * swp * 8;
-    if (lds > 160 * 1024)
+    if (lds + kLutBytes > 160 * 1024)
       return fail("zfp_hip: block size %u bits too large for LDS", p.cp.maxbits);
     Partial* parts = nullptr;
     if (g0) {
@@ -234,10 +235,10 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     if (p.vec)
       hipLaunchKernelGGL((encode3_aligned<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, d_out,
-                         sw, swp, g0, parts);
+                         sw, swp, magic, g0, parts);
     else
       hipLaunchKernelGGL((encode3_aligned<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, d_out,
-                         sw, swp, g0, parts);
+                         sw, swp, magic, g0, parts);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (g0) {
@@ -252,7 +253,7 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   // general path
   const uint32_t swp = (uint32_t)slot_words_odd(p.bound_bits);
   size_t lds = (size_t)kWavesPerGroup * (64 * swp + 64) * 8;
-  if (lds > 160 * 1024)
+  if (lds + kLutBytes > 160 * 1024)
     return fail("zfp_hip: block bound %u bits too large for LDS", p.bound_bits);
   const bool var = !p.fixed;
   // misc: [0] total bits, [1] ticket|error

@@ -287,12 +287,13 @@ __device__ __forceinline__ uint32_t encode_ints3(OrSlot& w, const uint32_t* lut,
 }
 
 template <typename Int>
-__device__ __forceinline__ uint32_t decode_ints3(WordReader& r, Int (&q)[64], uint32_t budget, uint32_t prec)
+__device__ __forceinline__ uint32_t decode_ints3(WordReader& r, const uint32_t* sq, Int (&q)[64], uint32_t budget,
+                                                 uint32_t prec)
 {
   using S = typename std::conditional<sizeof(Int) == 4, float, double>::type;
   constexpr int PREC = Traits<S>::kIntPrec;
   uint64_t P[PREC];
-  uint32_t used = decode_planes64<PREC>(r, budget, prec, P);
+  uint32_t used = decode_planes64<PREC>(r, sq, budget, prec, P);
   if constexpr (PREC == 32)
     coeffs_from_planes(q, P);
   else
@@ -305,10 +306,13 @@ __device__ __forceinline__ uint32_t decode_ints3(WordReader& r, Int (&q)[64], ui
 // sorts above inf, so one compare flags inf/NaN blocks), and for a finite
 // block with a finite scale s*x < 2^30 always, so the hardware conversion
 // matches C's.  Blocks holding inf/NaN or with a scale that overflows take the
-// exact path (NaN-ignoring max, x86 INT_MIN conversions); the branch is
-// uniform and skipped unless some lane in the wave needs it.
-__device__ __forceinline__ int lossy_emax_cast(int32_t (&q)[64], const float (&v)[64], const CodecParams& cp,
-                                               uint32_t& mp)
+// exact path (NaN-ignoring max, x86 INT_MIN conversions); that branch is
+// wave-uniform, taken only if some lane needs it, and re-reads the block
+// through `reload` so the inputs are dead after the fast cast (the cast is
+// done in place, keeping the register footprint at one block).
+template <typename Reload>
+__device__ __forceinline__ int lossy_emax_cast(int32_t (&q)[64], float (&v)[64], const CodecParams& cp,
+                                               uint32_t& mp, Reload&& reload)
 {
   int32_t mi = 0;
   uint32_t mu = 0;
@@ -325,19 +329,21 @@ __device__ __forceinline__ int lossy_emax_cast(int32_t (&q)[64], const float (&v
     emax = block_emax(block_absmax(v));
   mp = precision3(emax, cp);
   const bool cast = mp != 0 && emax != -127;
-  if (__any(cast && (bad || emax < -97))) {
-    fwd_cast(q, v, emax);
-  } else {
-    const float s = __uint_as_float((uint32_t)(157 - emax) << 23);
+  const float s = __uint_as_float((uint32_t)(157 - emax) << 23);
 #pragma unroll
-    for (int i = 0; i < 64; i++)
-      q[i] = (int32_t)(s * v[i]);
+  for (int i = 0; i < 64; i++)
+    q[i] = (int32_t)(s * v[i]);
+  if (__any(cast && (bad || emax < -97))) {
+    float w[64];
+    reload(w);
+    fwd_cast(q, w, emax);
   }
   return emax;
 }
 
-__device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], const double (&v)[64], const CodecParams& cp,
-                                               uint32_t& mp)
+template <typename Reload>
+__device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], double (&v)[64], const CodecParams& cp,
+                                               uint32_t& mp, Reload&&)
 {
   const int emax = block_emax(block_absmax(v));
   mp = precision3(emax, cp);
@@ -347,8 +353,9 @@ __device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], const double (&
 
 // Encode one block into a zeroed slot; returns its length in bits including
 // minbits padding (padding bits are the slot's zeros).
-template <typename S, bool REV>
-__device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut, S (&v)[64], const CodecParams& cp)
+template <typename S, bool REV, typename Reload>
+__device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut, S (&v)[64], const CodecParams& cp,
+                                                  Reload&& reload)
 {
   using T = Traits<S>;
   using Int = typename T::Int;
@@ -410,7 +417,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
   } else {
     // lossy (encodef.c:63-90)
     uint32_t mp;
-    const int emax = lossy_emax_cast(q, v, cp, mp);
+    const int emax = lossy_emax_cast(q, v, cp, mp, reload);
     const uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
     uint32_t bits = 1;
     if (e) {
@@ -430,7 +437,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
 
 // Decode one block; returns the number of bits consumed (incl. padding).
 template <typename S, bool REV>
-__device__ __forceinline__ uint32_t decode_block3(WordReader& r, S (&v)[64], const CodecParams& cp)
+__device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t* sq, S (&v)[64], const CodecParams& cp)
 {
   using T = Traits<S>;
   using Int = typename T::Int;
@@ -458,7 +465,7 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, S (&v)[64], con
     uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
     uint32_t maxb = cp.maxbits - bits;
     uint32_t prec = (uint32_t)r.read(T::kPbits) + 1;
-    uint32_t ib = T::kPbits + decode_ints3(r, q, maxb - T::kPbits, prec);
+    uint32_t ib = T::kPbits + decode_ints3(r, sq, q, maxb - T::kPbits, prec);
     if (ib < minb) {
       r.skip(minb - ib);
       ib = minb;
@@ -487,7 +494,7 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, S (&v)[64], con
     int emax = (int)r.read(kE) - T::kEbias;
     uint32_t mp = precision3(emax, cp);
     uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
-    uint32_t ib = decode_ints3(r, q, cp.maxbits - bits, mp);
+    uint32_t ib = decode_ints3(r, sq, q, cp.maxbits - bits, mp);
     if (ib < minb) {
       r.skip(minb - ib);
       ib = minb;

@@ -420,33 +420,60 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32])
 // then one OR of (verbatim | group << n) into the slot plus, for lanes whose
 // x reaches past bit 15, one OR per further 16-bit unit.  The budget is not
 // checked inside a plane: bits beyond it fall past the block end.
-__device__ __forceinline__ void code_plane(OrSlot& s, const uint32_t* lut, uint64_t plane, uint32_t& n, uint32_t& pos)
+//
+// The significance count after a plane is known as soon as its top one is,
+// so the loop is software-pipelined: plane k-1 is analysed and its table
+// look-ups issued before plane k's slot writes, and the look-up latency (LDS
+// ops complete in order, so a wait on a read also waits on earlier writes)
+// stays off the critical path.
+struct PlaneScan {
+  uint64_t x, xp;  // remaining bits, and with the top one cleared
+  uint32_t h, c;   // top one, popcount
+  uint32_t e0, e1; // table entries of xp's low two bytes
+  bool nz;
+};
+
+__device__ __forceinline__ PlaneScan scan_plane(const uint32_t* lut, uint64_t plane, uint32_t n)
 {
-  const bool part = n < 64;
+  PlaneScan r;
+  r.x = n < 64 ? plane >> (n & 63u) : 0ull;
+  r.nz = r.x != 0;
+  r.h = 63u - (uint32_t)__clzll((long long)(r.x | 1ull));
+  r.c = (uint32_t)__popcll(r.x);
+  r.xp = r.x & ~(1ull << r.h);
+  r.e0 = lut[(uint32_t)r.xp & 0xffu];
+  r.e1 = lut[((uint32_t)r.xp >> 8) & 0xffu];
+  return r;
+}
+
+__device__ __forceinline__ uint32_t next_sig(const PlaneScan& r, uint32_t n)
+{
+  return r.nz ? ((n + r.h == 63u) ? 64u : n + r.h + 1u) : n;
+}
+
+__device__ __forceinline__ void emit_plane(OrSlot& s, const uint32_t* lut, const PlaneScan& r, uint64_t plane,
+                                           uint32_t n, uint32_t& pos)
+{
   const uint32_t nn = n & 63u;
-  const uint64_t x = part ? plane >> nn : 0ull;
-  const uint64_t verb = plane ^ (x << nn);
-  const bool nz = x != 0;
-  const uint32_t h = 63u - (uint32_t)__clzll((long long)(x | 1ull));
-  const uint32_t c = (uint32_t)__popcll(x);
-  const uint64_t xp = x & ~(1ull << h);
-  const bool impl = nz && (n + h == 63u);
-  const bool normal = nz && !impl;
-  const uint32_t lr = nz ? h + c : 0u;
-  const uint32_t u0 = (uint32_t)xp & 0xffffu;
-  uint64_t grp = ((uint64_t)dbl16(lut, u0) << 1) | (nz ? 1ull : 0ull);
+  const uint64_t verb = plane ^ (r.x << nn);
+  const bool impl = r.nz && (n + r.h == 63u);
+  const bool normal = r.nz && !impl;
+  const uint32_t lr = r.nz ? r.h + r.c : 0u;
+  const uint32_t b0 = (uint32_t)r.xp & 0xffu;
+  const uint32_t d16 = r.e0 | (r.e1 << (8u + (uint32_t)__popc(b0)));
+  uint64_t grp = ((uint64_t)d16 << 1) | (r.nz ? 1ull : 0ull);
   if (normal && lr < 64)
     grp |= 1ull << lr;
-  const uint32_t glen = nz ? (impl ? lr : lr + 2u) : (part ? 1u : 0u);
+  const uint32_t glen = r.nz ? (impl ? lr : lr + 2u) : (n < 64 ? 1u : 0u);
   const uint64_t lo = verb | (grp << nn);
   const uint64_t hi = nn ? (grp >> (64 - nn)) : 0ull;
   s.put128(pos, lo, hi, n + glen);
-  if (__any(nz && h >= 16)) {
+  if (__any(r.nz && r.h >= 16)) {
     const uint32_t ps = pos + n;
-    uint32_t off = 17u + (uint32_t)__popc(u0);
+    uint32_t off = 17u + (uint32_t)__popc((uint32_t)r.xp & 0xffffu);
 #pragma unroll
     for (int j = 1; j < 4; j++) {
-      const uint32_t u = (uint32_t)(xp >> (16 * j)) & 0xffffu;
+      const uint32_t u = (uint32_t)(r.xp >> (16 * j)) & 0xffffu;
       if (__any(u != 0))
         s.put(ps + off, dbl16(lut, u), 32);  // u == 0 ORs zeros
       off += 16u + (uint32_t)__popc(u);
@@ -455,7 +482,6 @@ __device__ __forceinline__ void code_plane(OrSlot& s, const uint32_t* lut, uint6
       s.put(ps + lr, (normal && lr >= 64) ? 1ull : 0ull, 1);
   }
   pos += n + glen;
-  n = nz ? (impl ? 64u : n + h + 1u) : n;
 }
 
 // Codes planes PREC-1 .. PREC-maxprec starting at bit `pos` of the slot;
@@ -469,14 +495,21 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
 {
   const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
   uint32_t n = 0;
+  uint64_t plane = ((uint64_t)Ph[PREC - 1] << 32) | Pl[PREC - 1];
+  PlaneScan cur = scan_plane(lut, plane, 0);
   for (int k = PREC - 1; k >= 0; k--) {
     const bool act = pos < lim && (uint32_t)k >= kmin;
     if (!__any(act))
       break;
-    const int ku = __builtin_amdgcn_readfirstlane(k);
-    const uint64_t plane = ((uint64_t)Ph[ku] << 32) | Pl[ku];
+    const uint32_t nnext = next_sig(cur, n);
+    const int kn = __builtin_amdgcn_readfirstlane(k > 0 ? k - 1 : 0);
+    const uint64_t pnext = ((uint64_t)Ph[kn] << 32) | Pl[kn];
+    const PlaneScan nxt = scan_plane(lut, pnext, nnext);
     if (act)
-      code_plane(s, lut, plane, n, pos);
+      emit_plane(s, lut, cur, plane, n, pos);
+    n = nnext;
+    plane = pnext;
+    cur = nxt;
   }
   return pos < lim ? pos : lim;
 }
@@ -484,11 +517,36 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
 // Decoder twin (decode.c:69-246), including the reference quirk that a
 // positive group test sets the bit where the scan stopped even when the
 // budget ran out first.
-__device__ __forceinline__ uint64_t decode_plane64(WordReader& r, uint32_t& bits, uint32_t& n)
+//
+// Fast path (closed form).  After a "1" group test the section is a sequence
+// of tokens, one per coefficient position: "0" (zero), "11" (one, next test
+// positive), "10" (one, stop).  Every run of ones starts on a token boundary,
+// so the section ends at the first run of ones of ODD length, found without a
+// loop by the carry trick: adding 1 at the starts of runs that begin on even
+// (odd) bits carries past each run, and the carry lands on an odd (even) bit
+// exactly when the run is odd.  The ones of the plane are the first bits of the
+// pairs; squeezing those bits (bit p_i + i -> p_i) is one table look-up per
+// byte.  Lanes whose section does not end inside the next 63 bits, reaches the
+// implicit last coefficient, or is cut by the budget run the reference loop.
+constexpr uint64_t kEven = 0x5555555555555555ull;
+constexpr uint64_t kOdd = 0xaaaaaaaaaaaaaaaaull;
+
+// squeeze table: entry b has bit (l - r) set for the r-th one of b at bit l
+__device__ __forceinline__ uint32_t squeeze_entry(uint32_t b)
 {
-  uint32_t m = n < bits ? n : bits;
-  uint64_t x = r.read(m);
-  bits -= m;
+  uint32_t o = 0, r = 0;
+#pragma unroll
+  for (int l = 0; l < 8; l++) {
+    if ((b >> l) & 1u) {
+      o |= 1u << (l - r);
+      r++;
+    }
+  }
+  return o;
+}
+
+__device__ __forceinline__ void decode_group_slow(WordReader& r, uint64_t& x, uint32_t& bits, uint32_t& n)
+{
   while (bits && n < 64) {
     bits--;
     if (!r.read1())
@@ -509,31 +567,77 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, uint32_t& bits
     x |= 1ull << n;
     n++;
   }
+}
+
+__device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
+{
+  uint32_t m = n < bits ? n : bits;
+  uint64_t x = r.read(m);
+  bits -= m;
+  bool slow = false;
+  if (n < 64 && bits) {
+    const uint64_t w = r.peek64();
+    if (!(w & 1)) {
+      r.skip(1);
+      bits--;
+    } else {
+      const uint64_t S = w >> 1;
+      const uint64_t starts = S & ~(S << 1);
+      const uint64_t se = S + (starts & kEven), so = S + (starts & kOdd);
+      const uint64_t ends = ((se & ~S) & kOdd) | ((so & ~S) & kEven);
+      const uint32_t q = ctz64(ends);
+      const uint64_t mq = low_mask(q);
+      const uint32_t ones = (uint32_t)__popcll(S & mq);
+      const uint32_t P = q - (ones - 1) / 2;
+      if (ends != 0 && n + P <= 63 && q + 2 <= bits) {
+        uint64_t F = S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd));
+        uint64_t xx = 0;
+        uint32_t sh = 0;
+        while (__any(F != 0)) {
+          const uint32_t b = (uint32_t)F & 0xffu;
+          xx |= (uint64_t)sq[b] << sh;
+          sh += 8u - (uint32_t)__popc(b);
+          F >>= 8;
+        }
+        x |= xx << n;
+        n += P;
+        r.skip(q + 2);
+        bits -= q + 2;
+      } else {
+        slow = true;
+      }
+    }
+  }
+  if (slow)
+    decode_group_slow(r, x, bits, n);
   return x;
 }
 
 template <int K, int PREC>
 struct DecodePlanes {
-  static __device__ __forceinline__ void run(WordReader& r, uint64_t (&P)[PREC], uint32_t kmin, uint32_t& bits,
-                                             uint32_t& n)
+  static __device__ __forceinline__ void run(WordReader& r, const uint32_t* sq, uint64_t (&P)[PREC], uint32_t kmin,
+                                             uint32_t& bits, uint32_t& n)
   {
     bool act = bits != 0 && (uint32_t)K >= kmin;
     if (!__any(act))
       return;
     if (act)
-      P[K] = decode_plane64(r, bits, n);
-    DecodePlanes<K - 1, PREC>::run(r, P, kmin, bits, n);
+      P[K] = decode_plane64(r, sq, bits, n);
+    DecodePlanes<K - 1, PREC>::run(r, sq, P, kmin, bits, n);
   }
 };
 
 template <int PREC>
 struct DecodePlanes<-1, PREC> {
-  static __device__ __forceinline__ void run(WordReader&, uint64_t (&)[PREC], uint32_t, uint32_t&, uint32_t&) {}
+  static __device__ __forceinline__ void run(WordReader&, const uint32_t*, uint64_t (&)[PREC], uint32_t, uint32_t&,
+                                             uint32_t&)
+  {
+  }
 };
 
 template <int PREC>
-__device__ __forceinline__ uint32_t decode_planes64(WordReader& r, uint32_t budget, uint32_t maxprec,
-                                                    uint64_t (&P)[PREC])
+__device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_t* sq, uint32_t budget,
+                                                    uint32_t maxprec, uint64_t (&P)[PREC])
 {
   const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
   uint32_t bits = budget;
@@ -541,7 +645,7 @@ __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, uint32_t budg
 #pragma unroll
   for (int k = 0; k < PREC; k++)
     P[k] = 0;
-  DecodePlanes<PREC - 1, PREC>::run(r, P, kmin, bits, n);
+  DecodePlanes<PREC - 1, PREC>::run(r, sq, P, kmin, bits, n);
   return budget - bits;
 }
 

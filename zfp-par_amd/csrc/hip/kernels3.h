@@ -62,7 +62,7 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m
 // run's first and last words (shared with neighbouring waves) go to the
 // fix-up kernels.  Slots are swp >= sw + 1 words; word sw is the trash word.
 template <typename S, bool VEC, bool REV>
-__global__ __launch_bounds__(256) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
+__global__ __launch_bounds__(256, 4) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        uint64_t* __restrict__ out, uint32_t sw, uint32_t swp,
                                                        uint32_t magic, uint32_t r0, Partial* __restrict__ partials)
 {
@@ -80,7 +80,7 @@ __global__ __launch_bounds__(256) void encode3_aligned(const S* __restrict__ dat
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
     OrSlot os{wslot + (size_t)lane * swp, sw};
-    encode_block3<S, REV>(os, lut, v, cp);
+    encode_block3<S, REV>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
   if (first >= g.nblocks)
     return;
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
     OrSlot os{wbase + (size_t)lane * a.swp, a.swp - 1};
-    len = encode_block3<S, REV>(os, lut, v, cp);
+    len = encode_block3<S, REV>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
   const uint32_t incl = wave_incl_scan(len);
   const uint32_t excl_l = incl - len;
@@ -352,7 +352,9 @@ struct DecodeArgs {
 template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
 {
+  __shared__ uint32_t sq[256];
   extern __shared__ uint64_t lds[];
+  sq[threadIdx.x] = squeeze_entry(threadIdx.x);
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   uint64_t* seg = lds + (size_t)wv * a.seg_words;
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g,
   r.w = seg;
   r.pos = (G & 63) + pos;
   S v[64];
-  decode_block3<S, REV>(r, v, cp);
+  decode_block3<S, REV>(r, sq, v, cp);
   BlockPos p = block_pos(g, b, 3);
   scatter3<S, VEC>(v, data, g, p);
 }

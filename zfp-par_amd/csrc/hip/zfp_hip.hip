@@ -344,7 +344,7 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
     a.idx_base = index->d_base;
   }
   size_t lds = (size_t)kWavesPerGroup * a.seg_words * 8;
-  if (lds > 160 * 1024)
+  if (lds + kLutBytes > 160 * 1024)
     return fail("zfp_hip: block size too large for LDS staging (%u bits)", per_block);
   dim3 grid((unsigned)ngroups), block(256);
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));

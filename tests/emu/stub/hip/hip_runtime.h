@@ -1,0 +1,47 @@
+// Host (single-lane) stand-in for the HIP device API, so the device-side codec
+// headers compile with g++ for logic tests (tests/emu).  A "wave" is one lane:
+// __any(x) == x and readfirstlane is the identity.
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <type_traits>
+#define __device__
+#define __host__
+#define __global__
+#define __shared__ static
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+static inline int __any(int x) { return x != 0; }
+static inline int __popc(uint32_t x) { return __builtin_popcount(x); }
+static inline int __popcll(uint64_t x) { return __builtin_popcountll(x); }
+static inline int __clzll(long long x) { return x ? __builtin_clzll((uint64_t)x) : 64; }
+static inline uint32_t __float_as_uint(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
+static inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
+static inline long long __double_as_longlong(double d) { long long u; std::memcpy(&u, &d, 8); return u; }
+static inline double __longlong_as_double(long long u) { double d; std::memcpy(&d, &u, 8); return d; }
+static inline int __builtin_amdgcn_readfirstlane(int x) { return x; }
+// v_perm_b32: bytes 0-3 from src1, 4-7 from src0
+static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel)
+{
+  uint64_t v = ((uint64_t)s0 << 32) | s1;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; i++) {
+    uint32_t b = (sel >> (8 * i)) & 0xff;
+    r |= (uint32_t)((v >> (8 * (b & 7))) & 0xff) << (8 * i);
+  }
+  return r;
+}
+#define __ATOMIC_RELAXED_STUB 0
+#define __HIP_MEMORY_SCOPE_WAVEFRONT 1
+template <typename T> static inline T __hip_atomic_fetch_or(T* p, T v, int, int) { T o = *p; *p |= v; return o; }
+static inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
+struct float4 { float x, y, z, w; };
+struct double2 { double x, y; };
+static inline float4 make_float4(float a, float b, float c, float d) { return float4{a, b, c, d}; }
+static inline double2 make_double2(double a, double b) { return double2{a, b}; }
+#include <cmath>
+using std::fabs;
+#include <math.h>
+#include <algorithm>
+using std::max;
+using std::min;

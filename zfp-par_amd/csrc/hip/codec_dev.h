@@ -584,7 +584,9 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
       const uint64_t S = w >> 1;
       const uint64_t starts = S & ~(S << 1);
       const uint64_t se = S + (starts & kEven), so = S + (starts & kOdd);
-      const uint64_t ends = ((se & ~S) & kOdd) | ((so & ~S) & kEven);
+      // S holds 63 stream bits; its bit 63 is not data, so a run reaching
+      // bit 62 must not be taken as ended there
+      const uint64_t ends = (((se & ~S) & kOdd) | ((so & ~S) & kEven)) & ~(1ull << 63);
       const uint32_t q = ctz64(ends);
       const uint64_t mq = low_mask(q);
       const uint32_t ones = (uint32_t)__popcll(S & mq);

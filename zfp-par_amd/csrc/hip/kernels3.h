@@ -344,20 +344,27 @@ struct DecodeArgs {
   uint32_t g0;
   uint32_t var;
   uint32_t maxbits;
-  uint32_t seg_words;      // LDS words per wave
+  uint32_t W;              // words staged per block (block bound + 1)
+  uint32_t swp;            // LDS slot stride (odd, >= W)
+  uint32_t wmagic;         // ceil(2^32 / W)
   const uint16_t* idx_len;
   const uint64_t* idx_base;
 };
 
+// Each lane's block is staged into its own LDS slot (odd stride: lanes reading
+// the same offset of their blocks hit different banks), funnel-shifted so the
+// block starts at bit 0.  Staging is cooperative: thread t copies word j of
+// block l for t = l*W + j, so consecutive threads read consecutive stream words.
 template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
 {
   __shared__ uint32_t sq[256];
+  __shared__ uint32_t sbit[kWavesPerGroup * 64];
   extern __shared__ uint64_t lds[];
   sq[threadIdx.x] = squeeze_entry(threadIdx.x);
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  uint64_t* seg = lds + (size_t)wv * a.seg_words;
+  uint64_t* wslot = lds + (size_t)wv * 64 * a.swp;
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
   const uint64_t first = w * 64;
   const bool live = first < g.nblocks;
@@ -365,33 +372,40 @@ __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g,
   const bool act = b < g.nblocks;
 
   uint64_t start = 0;
-  uint32_t pos = 0, total = 0;
+  uint32_t pos = 0;
   if (!live) {
   } else if (a.var) {
     uint32_t len = act ? a.idx_len[b] : 0u;
     uint32_t incl = wave_incl_scan(len);
     pos = incl - len;
-    total = __shfl(incl, 63, 64);
     start = a.idx_base[w];
   } else {
-    uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
     pos = lane * a.maxbits;
-    total = (uint32_t)nb * a.maxbits;
     start = first * (uint64_t)a.maxbits;
   }
   const uint64_t G = a.g0 + start;
   const uint64_t W0 = G >> 6;
-  const uint32_t nw = (uint32_t)(((G + total + 63) >> 6) - W0 + 1);
-  for (uint32_t o = lane; live && o < nw && o < a.seg_words; o += 64) {
-    uint64_t gi = W0 + o;
-    seg[o] = gi < a.in_words ? a.in[gi] : 0ull;
+  sbit[threadIdx.x] = (uint32_t)(G & 63) + pos;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const uint64_t nb = live ? ((g.nblocks - first) < 64 ? (g.nblocks - first) : 64) : 0;
+  const uint32_t pairs = (uint32_t)nb * a.W;
+  for (uint32_t t = lane; t < pairs; t += 64) {
+    const uint32_t l = __umulhi(t, a.wmagic);
+    const uint32_t j = t - l * a.W;
+    const uint32_t sb = sbit[wv * 64 + l];
+    const uint64_t gw = W0 + (sb >> 6) + j;
+    const uint32_t sh = sb & 63;
+    const uint64_t lo = gw < a.in_words ? a.in[gw] : 0ull;
+    const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
+    wslot[(size_t)l * a.swp + j] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
   }
   __syncthreads();
   if (!act)
     return;
   WordReader r;
-  r.w = seg;
-  r.pos = (G & 63) + pos;
+  r.w = wslot + (size_t)lane * a.swp;
+  r.pos = 0;
   S v[64];
   decode_block3<S, REV>(r, sq, v, cp);
   BlockPos p = block_pos(g, b, 3);

@@ -338,13 +338,15 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
   a.var = p.fixed ? 0 : 1;
   a.maxbits = p.cp.maxbits;
   uint32_t per_block = p.fixed ? p.cp.maxbits : p.max_len;
-  a.seg_words = (uint32_t)((64ull * per_block + 63) / 64 + 2);
+  a.W = (per_block + 63) / 64 + 1;  // peek64 at the budget end reads one word past it
+  a.swp = a.W | 1;
+  a.wmagic = (uint32_t)((0x100000000ull + a.W - 1) / a.W);
   if (!p.fixed) {
     a.idx_len = index->d_len;
     a.idx_base = index->d_base;
   }
-  size_t lds = (size_t)kWavesPerGroup * a.seg_words * 8;
-  if (lds + kLutBytes > 160 * 1024)
+  size_t lds = (size_t)kWavesPerGroup * 64 * a.swp * 8;
+  if (lds + kLutBytes + kWavesPerGroup * 64 * 4 > 160 * 1024)
     return fail("zfp_hip: block size too large for LDS staging (%u bits)", per_block);
   dim3 grid((unsigned)ngroups), block(256);
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));

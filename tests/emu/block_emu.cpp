@@ -38,13 +38,13 @@ static int run(const CodecParams& cp, int type, std::mt19937_64& rng, int trials
     j.s[0] = 1, j.s[1] = 4, j.s[2] = 16;
     std::vector<uint64_t> ow(600, 0), slot(600, 0);
     uint64_t oend = oz_compress(&j, orig, ow.data(), 0);
-    OrSlot os{slot.data(), 590};
+    OrSlot os{slot.data(), 1199};
     uint32_t len = encode_block3<S, false>(os, lut, v, cp, [&](S (&r)[64]) { for (int i = 0; i < 64; i++) r[i] = orig[i]; });
     if (cp.minexp < kMinExp) {
       S v2[64];
       for (int i = 0; i < 64; i++) v2[i] = orig[i];
       std::fill(slot.begin(), slot.end(), 0);
-      OrSlot os2{slot.data(), 590};
+      OrSlot os2{slot.data(), 1199};
       len = encode_block3<S, true>(os2, lut, v2, cp, [&](S (&r)[64]) { for (int i = 0; i < 64; i++) r[i] = orig[i]; });
     }
     bool ok = len == oend;
@@ -54,9 +54,12 @@ static int run(const CodecParams& cp, int type, std::mt19937_64& rng, int trials
     }
     // decode the oracle's words
     S d[64], od[64];
+    const bool any_all = emu_any_all;
+    emu_any_all = false;  // decoder loops gate on __any; run them as a lone lane
     WordReader r{ow.data(), 0};
     uint32_t used = (cp.minexp < kMinExp) ? decode_block3<S, true>(r, sq, d, cp) : decode_block3<S, false>(r, sq, d, cp);
     oz_decompress(&j, od, ow.data(), 0);
+    emu_any_all = any_all;
     bool dok = used == oend && std::memcmp(d, od, sizeof d) == 0;
     if (!ok || !dok) {
       if (bad++ < 3)
@@ -82,12 +85,15 @@ int main()
     {"reversible", {1, 16658, 64, -1075}, {1, 16658, 64, -1075}},
     {"expert", {700, 900, 40, -60}, {700, 900, 40, -60}},
   };
-  for (auto& m : modes) {
-    char nm[64];
-    snprintf(nm, sizeof nm, "f32 %s", m.n);
-    bad += run<float>(m.f, 3, rng, 3000, nm);
-    snprintf(nm, sizeof nm, "f64 %s", m.n);
-    bad += run<double>(m.d, 4, rng, 3000, nm);
+  for (int all : {0, 1}) {  // 1: every wave-level branch of the encoder entered
+    emu_any_all = all;
+    for (auto& m : modes) {
+      char nm[64];
+      snprintf(nm, sizeof nm, "f32 %s%s", m.n, all ? " any" : "");
+      bad += run<float>(m.f, 3, rng, 3000, nm);
+      snprintf(nm, sizeof nm, "f64 %s%s", m.n, all ? " any" : "");
+      bad += run<double>(m.d, 4, rng, 3000, nm);
+    }
   }
   return bad != 0;
 }

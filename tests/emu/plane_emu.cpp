@@ -1,0 +1,95 @@
+// Plane coder (codec_dev.h code_planes) against a literal restatement of the
+// reference's embedded coder (src/template/encode.c:92-132, encode_few_ints):
+// adversarial plane patterns -- all-ones 16-bit units, tops at bit 63, long
+// jumps of significance, budgets cut at every offset -- for 32 and 64 planes.
+#include <cstdio>
+#include <cstring>
+#include <random>
+#include <vector>
+#include "codec_dev.h"
+using namespace zfp_amd;
+
+// reference: encode.c:92-132 with a 64-bit LSB-first writer
+static uint32_t ref_code(std::vector<uint64_t>& w, uint32_t pos0, uint32_t maxbits, uint32_t maxprec,
+                         const uint64_t* planes, int prec)
+{
+  uint32_t kmin = (uint32_t)prec > maxprec ? prec - maxprec : 0;
+  uint32_t bits = maxbits, n = 0, pos = pos0;
+  auto put = [&](uint32_t b) { if (b) w[pos >> 6] |= 1ull << (pos & 63); pos++; return b; };
+  for (uint32_t k = prec; bits && k-- > kmin;) {
+    uint64_t x = planes[k];
+    uint32_t m = n < bits ? n : bits;
+    bits -= m;
+    for (uint32_t i = 0; i < m; i++) put((x >> i) & 1);
+    x = m < 64 ? x >> m : 0;
+    for (; bits && n < 64; x >>= 1, n++) {
+      bits--;
+      if (put(x != 0)) {
+        for (; bits && n < 63; x >>= 1, n++) {
+          bits--;
+          if (put(x & 1u)) break;
+        }
+      } else
+        break;
+    }
+  }
+  return pos - pos0;
+}
+
+template <int PREC>
+static int run(std::mt19937_64& rng, int trials)
+{
+  uint32_t lut[256];
+  for (int b = 0; b < 256; b++) lut[b] = dbl_entry(b);
+  int bad = 0;
+  for (int t = 0; t < trials; t++) {
+    uint64_t P[PREC];
+    int kind = t % 7;
+    for (int k = 0; k < PREC; k++) {
+      uint64_t r = rng();
+      switch (kind) {
+        case 0: P[k] = r; break;                                      // dense
+        case 1: P[k] = (rng() % 4 == 0) ? r & rng() & rng() : 0; break;  // sparse
+        case 2: P[k] = (k == PREC - 1 - (int)(t % 5)) ? 0xffffull << (16 * (rng() % 4)) : r & 0xffff0000ffffull; break;
+        case 3: P[k] = (rng() % 3 == 0) ? (1ull << 63) | (r & 0xffff) : (r & 0x00ff00ff00ff00ffull); break;
+        case 4: P[k] = (k % 9 == 0) ? ~0ull : 0; break;
+        case 5: P[k] = (k == PREC - 2) ? (r | (1ull << (rng() % 64))) >> (rng() % 40) : r >> (rng() % 64); break;
+        default: P[k] = (k > PREC - 4) ? (1ull << (rng() % 64)) : r & (r >> 3); break;
+      }
+    }
+    uint32_t Pl[PREC], Ph[PREC];
+    for (int k = 0; k < PREC; k++) Pl[k] = (uint32_t)P[k], Ph[k] = (uint32_t)(P[k] >> 32);
+    const uint32_t pos0 = 1 + (uint32_t)(rng() % 40);
+    const uint32_t budgets[3] = {4096 * 2, 64 + (uint32_t)(rng() % 2000), 1 + (uint32_t)(rng() % 300)};
+    for (uint32_t lim_bits : budgets) {
+      uint32_t maxprec = (t % 3 == 0) ? 1 + (uint32_t)(rng() % PREC) : 64;
+      std::vector<uint64_t> rw(200, 0), slot(200, 0);
+      uint32_t rlen = ref_code(rw, pos0, lim_bits, maxprec, P, PREC);
+      OrSlot os{slot.data(), 399};
+      uint32_t end = code_planes<PREC>(os, lut, pos0, pos0 + lim_bits, maxprec, Pl, Ph);
+      bool ok = end - pos0 == rlen;
+      uint32_t e = pos0 + rlen;
+      for (uint32_t i = 0; ok && i < (e + 63) / 64; i++) {
+        uint64_t m = (i == e / 64 && (e & 63)) ? ((1ull << (e & 63)) - 1) : ~0ull;
+        ok = (slot[i] & m) == (rw[i] & m);
+      }
+      if (!ok && bad++ < 5)
+        printf("PREC %d trial %d kind %d lim %u maxprec %u: len %u vs ref %u\n", PREC, t, kind, lim_bits, maxprec,
+               end - pos0, rlen);
+    }
+  }
+  printf("planes%d mismatches %d\n", PREC, bad);
+  return bad;
+}
+
+int main()
+{
+  std::mt19937_64 rng(12345);
+  int bad = 0;
+  for (int all : {0, 1}) {  // 1: every wave-level branch entered (other lanes need it)
+    emu_any_all = all;
+    bad += run<32>(rng, 20000) + run<64>(rng, 10000);
+  }
+  printf("mismatches %d\n", bad);
+  return bad != 0;
+}

@@ -1,6 +1,6 @@
 // Host (single-lane) stand-in for the HIP device API, so the device-side codec
 // headers compile with g++ for logic tests (tests/emu).  A "wave" is one lane:
-// __any(x) == x and readfirstlane is the identity.
+// __any(x) == x (or true, see emu_any_all) and readfirstlane is the identity.
 #pragma once
 #include <cstdint>
 #include <cstring>
@@ -11,7 +11,10 @@
 #define __shared__ static
 #define __forceinline__ inline
 #define __launch_bounds__(...)
-static inline int __any(int x) { return x != 0; }
+// With emu_any_all set, every wave-level test passes as if some other lane
+// needed the branch: per-lane predication inside such branches is exercised.
+inline bool emu_any_all = false;
+static inline int __any(int x) { return x != 0 || emu_any_all; }
 static inline int __popc(uint32_t x) { return __builtin_popcount(x); }
 static inline int __popcll(uint64_t x) { return __builtin_popcountll(x); }
 static inline int __clzll(long long x) { return x ? __builtin_clzll((uint64_t)x) : 64; }
@@ -20,6 +23,11 @@ static inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4
 static inline long long __double_as_longlong(double d) { long long u; std::memcpy(&u, &d, 8); return u; }
 static inline double __longlong_as_double(long long u) { double d; std::memcpy(&d, &u, 8); return d; }
 static inline int __builtin_amdgcn_readfirstlane(int x) { return x; }
+// v_alignbit_b32: ({a,b} >> (c & 31)) low 32 bits
+static inline uint32_t __builtin_amdgcn_alignbit(uint32_t a, uint32_t b, uint32_t c)
+{
+  return (uint32_t)((((uint64_t)a << 32) | b) >> (c & 31));
+}
 // v_perm_b32: bytes 0-3 from src1, 4-7 from src0
 static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel)
 {

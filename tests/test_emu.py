@@ -45,4 +45,11 @@ def test_block_codec_matches_oracle_all_modes(oracle_obj):
     d, obj = oracle_obj
     r = subprocess.run([_build(d, "block_emu.cpp", [obj])], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
-    assert r.stdout.count(" 0/3000 bad") == 16, r.stdout
+    assert r.stdout.count(" 0/3000 bad") == 32, r.stdout
+
+
+def test_plane_coder_matches_reference_loop(tmp_path):
+    """code_planes vs a literal restatement of encode.c:92-132 on adversarial planes."""
+    r = subprocess.run([_build(str(tmp_path), "plane_emu.cpp")], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "mismatches 0" in r.stdout

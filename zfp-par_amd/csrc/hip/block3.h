@@ -386,7 +386,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
         // a single 0 bit (already zero in the slot)
         return 1u < cp.minbits ? cp.minbits : 1u;
       }
-      w.put(0, 1u | ((uint64_t)e << 2), 2 + kE);
+      w.head(1u | (e << 2));
       bits = 2 + kE;
     } else {
 #pragma unroll
@@ -394,7 +394,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
         Int x = (Int)bits_of(v[i]);
         q[i] = x < 0 ? (Int)((UInt)x ^ T::kTcMask) : x;
       }
-      w.put(0, 3, 2);
+      w.head(3u);
       bits = 2;
     }
     // rev_encode_block_<Int> (revencode.c:54-76)
@@ -409,7 +409,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
                         : 0u;
     if (prec > cp.maxprec) prec = cp.maxprec;
     if (prec < 1) prec = 1;
-    w.put(bits, prec - 1, T::kPbits);
+    w.put32(bits, prec - 1);
     const uint32_t end = encode_ints3(w, lut, q, bits + T::kPbits, cp.maxbits, prec);
     uint32_t ib = end - bits;
     if (ib < minb) ib = minb;
@@ -421,7 +421,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
     const uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
     uint32_t bits = 1;
     if (e) {
-      w.put(0, 2 * (uint64_t)e + 1, 1 + kE);
+      w.head(2 * e + 1);
       bits += kE;
       xform<3, false, false>(q);
       const uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);

@@ -69,40 +69,70 @@ __device__ __forceinline__ uint32_t ctz64(uint64_t x)
 // Encoder output: a per-lane slot of 64-bit words in LDS, zeroed before the
 // block is coded.  Bits are ORed in at their absolute position (LSB first,
 // bitstream.inl:289-313 word layout), so no write depends on an earlier one
-// and the coder needs no serial accumulator.  Positions past the block's
-// budget are garbage by construction: every word index is clamped to a trash
-// word (`trash`) that is never read, and readers mask at the block length.
+// and the coder needs no serial accumulator.  Bits past the block's budget
+// land in spare words at the slot's end (sized by slot_words_for) that are
+// never read; readers mask at the block length.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void lds_or(uint64_t* p, uint64_t v)
+__device__ __forceinline__ void lds_or32(uint32_t* p, uint32_t v)
 {
   __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// Writes are dword-granular funnel shifts (v_alignbit_b32: one full-rate op per
+// output dword; a 64-bit shift costs about three).  A value placed at bit p
+// (p >= 1) starts in dword j-1 with j = ceil(p / 32), at offset s = p - 32(j-1)
+// in [1, 32]; dword j-1+i receives ((v << s) >> 32 i), which is
+// alignbit(v_i, v_{i-1}, -p) since alignbit shifts by its operand mod 32.
 struct OrSlot {
-  uint64_t* w;
-  uint32_t trash;
+  uint64_t* w;    // slot base (bit 0 = bit 0 of w[0])
+  uint32_t jmax;  // last dword index of the slot (clamp target of put*_clamped)
 
-  __device__ __forceinline__ void or_word(uint32_t i, uint64_t v) { lds_or(w + (i < trash ? i : trash), v); }
-  // v < 2^len, len <= 64
-  __device__ __forceinline__ void put(uint32_t p, uint64_t v, uint32_t len)
+  __device__ __forceinline__ uint32_t* d() const { return reinterpret_cast<uint32_t*>(w); }
+  // block header bits at bit 0 (v < 2^32)
+  __device__ __forceinline__ void head(uint32_t v) { lds_or32(d(), v); }
+  // v1:v0 at bit p >= 1: dwords j-1 .. j+1
+  __device__ __forceinline__ void put64(uint32_t p, uint32_t v0, uint32_t v1)
   {
-    const uint32_t i = p >> 6, sh = p & 63;
-    or_word(i, v << sh);
-    if (__any(sh + len > 64))
-      or_word(i + 1, (v >> 1) >> (63 - sh));
+    uint32_t* q = d() + ((p + 31u) >> 5) - 1;
+    const uint32_t t = 0u - p;
+    lds_or32(q, __builtin_amdgcn_alignbit(v0, 0u, t));
+    lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
+    lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
   }
-  // (lo | hi << 64) < 2^len, len <= 128.  The spill words are written under
-  // wave-uniform tests (a lane with nothing to spill ORs a zero).
-  __device__ __forceinline__ void put128(uint32_t p, uint64_t lo, uint64_t hi, uint32_t len)
+  // v (32 bits) at bit p >= 1: dwords j-1, j
+  __device__ __forceinline__ void put32(uint32_t p, uint32_t v)
   {
-    const uint32_t i = p >> 6, sh = p & 63;
-    or_word(i, lo << sh);
-    if (__any(sh + len > 64))
-      or_word(i + 1, ((lo >> 1) >> (63 - sh)) | (hi << sh));
-    if (__any(sh + len > 128))
-      or_word(i + 2, (hi >> 1) >> (63 - sh));
+    uint32_t* q = d() + ((p + 31u) >> 5) - 1;
+    const uint32_t t = 0u - p;
+    lds_or32(q, __builtin_amdgcn_alignbit(v, 0u, t));
+    lds_or32(q + 1, __builtin_amdgcn_alignbit(0u, v, t));
+  }
+  // as put64, with the dwords clamped into the slot (bits past the budget)
+  __device__ __forceinline__ void put64_clamped(uint32_t p, uint32_t v0, uint32_t v1)
+  {
+    uint32_t j = (p + 31u) >> 5;
+    j = j < jmax - 1 ? j : jmax - 1;
+    uint32_t* q = d() + j - 1;
+    const uint32_t t = 0u - p;
+    lds_or32(q, __builtin_amdgcn_alignbit(v0, 0u, t));
+    lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
+    lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
+  }
+  __device__ __forceinline__ void put32_clamped(uint32_t p, uint32_t v)
+  {
+    uint32_t j = (p + 31u) >> 5;
+    j = j < jmax ? j : jmax;
+    uint32_t* q = d() + j - 1;
+    const uint32_t t = 0u - p;
+    lds_or32(q, __builtin_amdgcn_alignbit(v, 0u, t));
+    lds_or32(q + 1, __builtin_amdgcn_alignbit(0u, v, t));
   }
 };
+
+// Slot size (64-bit words) for a block budget of `lim` bits: a plane that starts
+// before lim writes its verbatim bits through dword ceil((lim-1)/32)+1 and its
+// group bits through dword ceil((lim+63)/32); group extensions are clamped.
+__host__ __device__ constexpr uint32_t slot_words_for(uint32_t lim) { return ((lim + 63u + 31u) / 32u) / 2u + 1u; }
 
 // Doubled-ones table: entry b holds the 8 bits of b LSB first with every one
 // written twice ("1" -> "11", "0" -> "0"), 8 + popcount(b) bits.  The group
@@ -123,7 +153,7 @@ __device__ __forceinline__ uint32_t dbl_entry(uint32_t b)
   return d;
 }
 
-// expansion of a 16-bit unit: 16 + popcount(u) bits
+// expansion of a 16-bit unit: 16 + popcount(u) <= 32 bits
 __device__ __forceinline__ uint32_t dbl16(const uint32_t* lut, uint32_t u)
 {
   const uint32_t b0 = u & 0xffu, b1 = (u >> 8) & 0xffu;
@@ -409,107 +439,91 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32])
 // run anywhere: exactly the reference's bit-by-bit truncation.
 // ---------------------------------------------------------------------------
 //
-// Closed form of one plane.  With n significant coefficients, x = plane >> n
-// (the not-yet-significant bits), h its highest one and c its popcount, the
-// reference's group tests emit "1", then for every bit of x up to h the bit
-// itself plus, after a one, the next group test's "1" -- i.e. "1" followed by
-// the doubled-ones expansion of x[0..h] with its final bit dropped -- then a
-// "0" test if n + h + 1 < 64 (otherwise the last one is implicit).  Clearing
-// the top one (x') makes the expansion garbage-free: "1" + dbl(x') is exact for
-// h + c bits and the final "1 0" (or nothing) is added as a tail.  A plane is
-// then one OR of (verbatim | group << n) into the slot plus, for lanes whose
-// x reaches past bit 15, one OR per further 16-bit unit.  The budget is not
-// checked inside a plane: bits beyond it fall past the block end.
+// Closed form of one plane.  With n significant coefficients (mask S = the low
+// n bits), N = plane & ~S holds the not-yet-significant ones; let h be the top
+// one of xs = N >> n and c = popcount(N).  The reference's group tests
+// (encode.c:92-132) emit "1", then every bit of xs up to h, each one followed by
+// the next test's "1" -- the doubled-ones expansion dbl(xs) -- except that the
+// top one's test is "0" (and both the top one and its test are implicit when
+// it is coefficient 63); an empty N emits a single "0" (none when n == 64).
+// So the group bits are g = [N != 0] | dbl(xs) << 1 minus the top pair's
+// surplus: (2 + implicit) << (h + c).  The plane's length is
+// n' + c + 1 - [n' == 64] - implicit with n' = bitlen(S | N).  One table look-up
+// per byte gives dbl; lanes whose xs reaches past bit 15 (at most three planes
+// per block) add the remaining 16-bit units in a wave-uniform branch.  The
+// budget is not checked inside a plane: bits beyond it fall past the block end
+// into the slot's spare words.
 //
-// The significance count after a plane is known as soon as its top one is,
-// so the loop is software-pipelined: plane k-1 is analysed and its table
-// look-ups issued before plane k's slot writes, and the look-up latency (LDS
-// ops complete in order, so a wait on a read also waits on earlier writes)
-// stays off the critical path.
-struct PlaneScan {
-  uint64_t x, xp;  // remaining bits, and with the top one cleared
-  uint32_t h, c;   // top one, popcount
-  uint32_t e0, e1; // table entries of xp's low two bytes
-  bool nz;
-};
-
-__device__ __forceinline__ PlaneScan scan_plane(const uint32_t* lut, uint64_t plane, uint32_t n)
-{
-  PlaneScan r;
-  r.x = n < 64 ? plane >> (n & 63u) : 0ull;
-  r.nz = r.x != 0;
-  r.h = 63u - (uint32_t)__clzll((long long)(r.x | 1ull));
-  r.c = (uint32_t)__popcll(r.x);
-  r.xp = r.x & ~(1ull << r.h);
-  r.e0 = lut[(uint32_t)r.xp & 0xffu];
-  r.e1 = lut[((uint32_t)r.xp >> 8) & 0xffu];
-  return r;
-}
-
-__device__ __forceinline__ uint32_t next_sig(const PlaneScan& r, uint32_t n)
-{
-  return r.nz ? ((n + r.h == 63u) ? 64u : n + r.h + 1u) : n;
-}
-
-__device__ __forceinline__ void emit_plane(OrSlot& s, const uint32_t* lut, const PlaneScan& r, uint64_t plane,
-                                           uint32_t n, uint32_t& pos)
-{
-  const uint32_t nn = n & 63u;
-  const uint64_t verb = plane ^ (r.x << nn);
-  const bool impl = r.nz && (n + r.h == 63u);
-  const bool normal = r.nz && !impl;
-  const uint32_t lr = r.nz ? r.h + r.c : 0u;
-  const uint32_t b0 = (uint32_t)r.xp & 0xffu;
-  const uint32_t d16 = r.e0 | (r.e1 << (8u + (uint32_t)__popc(b0)));
-  uint64_t grp = ((uint64_t)d16 << 1) | (r.nz ? 1ull : 0ull);
-  if (normal && lr < 64)
-    grp |= 1ull << lr;
-  const uint32_t glen = r.nz ? (impl ? lr : lr + 2u) : (n < 64 ? 1u : 0u);
-  const uint64_t lo = verb | (grp << nn);
-  const uint64_t hi = nn ? (grp >> (64 - nn)) : 0ull;
-  s.put128(pos, lo, hi, n + glen);
-  if (__any(r.nz && r.h >= 16)) {
-    const uint32_t ps = pos + n;
-    uint32_t off = 17u + (uint32_t)__popc((uint32_t)r.xp & 0xffffu);
-#pragma unroll
-    for (int j = 1; j < 4; j++) {
-      const uint32_t u = (uint32_t)(r.xp >> (16 * j)) & 0xffffu;
-      if (__any(u != 0))
-        s.put(ps + off, dbl16(lut, u), 32);  // u == 0 ORs zeros
-      off += 16u + (uint32_t)__popc(u);
-    }
-    if (__any(normal && lr >= 64))
-      s.put(ps + lr, (normal && lr >= 64) ? 1ull : 0ull, 1);
-  }
-  pos += n + glen;
-}
-
-// Codes planes PREC-1 .. PREC-maxprec starting at bit `pos` of the slot;
-// returns the end position clamped to `lim` (the block's bit budget end).
-// The plane index is wave-uniform, so Pl[k]/Ph[k] are register reads with a
-// scalar index (no unrolling: one copy of the plane code).
+// Codes planes PREC-1 .. PREC-maxprec starting at bit `pos` (>= 1) of the slot;
+// returns the end position clamped to `lim` (the block's bit budget end).  The
+// plane index is wave-uniform, so Pl[k]/Ph[k] are register reads with a scalar
+// index.
 template <int PREC>
 __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, uint32_t pos, uint32_t lim,
                                                 uint32_t maxprec, const uint32_t (&Pl)[PREC],
                                                 const uint32_t (&Ph)[PREC])
 {
   const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
-  uint32_t n = 0;
-  uint64_t plane = ((uint64_t)Ph[PREC - 1] << 32) | Pl[PREC - 1];
-  PlaneScan cur = scan_plane(lut, plane, 0);
+  uint32_t n = 0, Sl = 0, Sh = 0;
   for (int k = PREC - 1; k >= 0; k--) {
     const bool act = pos < lim && (uint32_t)k >= kmin;
     if (!__any(act))
       break;
-    const uint32_t nnext = next_sig(cur, n);
-    const int kn = __builtin_amdgcn_readfirstlane(k > 0 ? k - 1 : 0);
-    const uint64_t pnext = ((uint64_t)Ph[kn] << 32) | Pl[kn];
-    const PlaneScan nxt = scan_plane(lut, pnext, nnext);
-    if (act)
-      emit_plane(s, lut, cur, plane, n, pos);
-    n = nnext;
-    plane = pnext;
-    cur = nxt;
+    const int ku = __builtin_amdgcn_readfirstlane(k);
+    const uint32_t pl = Pl[ku], ph = Ph[ku];
+    const uint32_t Nl = pl & ~Sl, Nh = ph & ~Sh;
+    const uint64_t N = ((uint64_t)Nh << 32) | Nl;
+    const bool nz = N != 0;
+    const uint32_t clz = (uint32_t)__clzll((long long)(N | 1ull));  // of N when nz
+    const uint32_t n1 = nz ? 64u - clz : n;
+    const uint64_t S1 = nz ? (~0ull >> clz) : (((uint64_t)Sh << 32) | Sl);
+    const uint32_t t2 = (uint32_t)__popc(Nh) + (uint32_t)__popc(Nl) + n1;  // n' + c
+    const uint32_t impl = Nh >> 31;                                       // top one is coefficient 63
+    const uint32_t len = t2 + 1u - (uint32_t)(S1 >> 63) - impl;
+    const uint64_t xs = N >> (n & 63u);  // n == 64 only with N == 0
+    const uint32_t x0 = (uint32_t)xs;
+    const uint32_t b0 = x0 & 0xffu;
+    const uint32_t d16 = lut[b0] | (lut[(x0 >> 8) & 0xffu] << (8u + (uint32_t)__popc(b0)));
+    const uint32_t m = (2u + impl) << ((t2 - n - 1u) & 31u);
+    uint32_t g = ((d16 << 1) | (nz ? 1u : 0u)) - m;
+    const uint32_t h = n1 - n - 1u;  // top one of xs (when nz)
+    const bool ext = act && nz && h >= 16u;
+    if (__any(ext)) {
+      // the top one lies beyond the first unit: undo the surplus removal and
+      // expand units 1..3 at their dbl offsets
+      const uint32_t gp = pos + n;
+      uint32_t D = 16u + (uint32_t)__popc(x0 & 0xffffu);  // dbl length of unit 0
+      if (ext)
+        g += m;
+#pragma unroll
+      for (int j = 1; j < 4; j++) {
+        // lanes whose top one lies below this unit take no part (the branch is
+        // entered for the wave, so every per-lane effect is predicated here)
+        const bool unit = ext && h >= 16u * j;
+        if (__any(unit)) {
+          const uint32_t u = (uint32_t)(xs >> (16 * j)) & 0xffffu;
+          const uint32_t cu = (uint32_t)__popc(u);
+          uint32_t dj = dbl16(lut, u);
+          if (h < 16u * (j + 1))  // the top one is in this unit
+            dj -= (2u + impl) << ((h - 16u * j + cu - 1u) & 31u);
+          if (unit) {
+            if (j == 1)  // also carries bit 32 of g (unit 0 all ones)
+              s.put64_clamped(gp + D, (dj << 1) | (d16 >> 31), dj >> 31);
+            else
+              s.put32_clamped(gp + 1u + D, dj);
+          }
+          D += 16u + cu;
+        }
+      }
+    }
+    if (act) {
+      s.put64(pos, pl ^ Nl, ph ^ Nh);  // the n verbatim bits
+      s.put32(pos + n, g);
+      pos += len;
+      n = n1;
+      Sl = (uint32_t)S1;
+      Sh = (uint32_t)(S1 >> 32);
+    }
   }
   return pos < lim ? pos : lim;
 }

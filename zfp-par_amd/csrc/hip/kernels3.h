@@ -1,6 +1,7 @@
 // 3D encode/decode kernels: one block per lane, 4 independent waves per
 // 256-thread workgroup, each wave owning 64 consecutive blocks (raster order of
-// the chunk box, compress.c:86-94) and a private LDS region.
+// the chunk box, compress.c:86-94) and a private LDS region of per-lane slots
+// (slot_words_for(budget) words each, odd stride).
 //
 //  encode3_aligned  fixed rate with every block starting on a 64-bit word:
 //                   lane slots in LDS are copied out as one contiguous run.
@@ -60,7 +61,8 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m
 // blocks form one contiguous run of words; with a stream offset r0 = g0
 // (mod 64) != 0 every output word is a funnel shift of two run words, and the
 // run's first and last words (shared with neighbouring waves) go to the
-// fix-up kernels.  Slots are swp >= sw + 1 words; word sw is the trash word.
+// fix-up kernels.  Slots are swp >= slot_words_for(64 sw) words; words from sw
+// on are spare (bits past the budget) and never copied.
 template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256, 4) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        uint64_t* __restrict__ out, uint32_t sw, uint32_t swp,
@@ -79,7 +81,7 @@ __global__ __launch_bounds__(256, 4) void encode3_aligned(const S* __restrict__ 
     S v[64];
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
-    OrSlot os{wslot + (size_t)lane * swp, sw};
+    OrSlot os{wslot + (size_t)lane * swp, 2 * swp - 1};
     encode_block3<S, REV>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
   if (first >= g.nblocks)
@@ -230,14 +232,16 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
     S v[64];
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
-    OrSlot os{wbase + (size_t)lane * a.swp, a.swp - 1};
+    OrSlot os{wbase + (size_t)lane * a.swp, 2 * a.swp - 1};
     len = encode_block3<S, REV>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
   const uint32_t incl = wave_incl_scan(len);
   const uint32_t excl_l = incl - len;
   const uint32_t total = __shfl(incl, 63, 64);
   off[lane] = excl_l;
-  wrt[lane] = len < 64 * (a.swp - 1) ? len : 64 * (a.swp - 1);  // beyond: padding zeros
+  // bits below the budget are exact (past it the slot holds spill); beyond the
+  // slot a block can only hold minbits padding zeros
+  wrt[lane] = len < 64 * a.swp ? len : 64 * a.swp;
 
   uint64_t start = 0;  // bit offset of the wave's first block relative to g0
   if (!live) {

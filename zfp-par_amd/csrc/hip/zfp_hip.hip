@@ -204,8 +204,7 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
 
 static size_t slot_words_odd(uint32_t bits)
 {
-  size_t w = (bits + 63) / 64 + 1;
-  return w | 1;
+  return slot_words_for(bits) | 1;  // odd stride: fewer LDS bank collisions between lanes
 }
 
 // ---------------------------------------------------------------------------
@@ -221,7 +220,7 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   dim3 grid((unsigned)ngroups), block(256);
   if (p.fixed && (p.cp.maxbits % 64) == 0) {
     const uint32_t sw = p.cp.maxbits / 64;
-    const uint32_t swp = (sw + 1) | 1;  // odd stride, word sw is the trash word
+    const uint32_t swp = (uint32_t)slot_words_odd(p.cp.maxbits);  // words from sw on are spare
     const uint32_t magic = sw > 1 ? (uint32_t)((0x100000000ull + sw - 1) / sw) : 0u;
     size_t lds = (size_t)kWavesPerGroup * 64 * swp * 8;
     if (lds + kLutBytes > 160 * 1024)

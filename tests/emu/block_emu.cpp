@@ -46,6 +46,20 @@ static int run(const CodecParams& cp, int type, std::mt19937_64& rng, int trials
       std::fill(slot.begin(), slot.end(), 0);
       OrSlot os2{slot.data(), 1199};
       len = encode_block3<S, true>(os2, lut, v2, cp, [&](S (&r)[64]) { for (int i = 0; i < 64; i++) r[i] = orig[i]; });
+    } else if (cp.minbits == cp.maxbits && cp.maxprec >= 64) {
+      // fixed-rate specialisation (the aligned kernel's coder)
+      S v2[64];
+      for (int i = 0; i < 64; i++) v2[i] = orig[i];
+      std::vector<uint64_t> slot2(600, 0);
+      OrSlot os2{slot2.data(), 1199};
+      uint32_t len2 = encode_block3<S, false, true>(os2, lut, v2, cp, [&](S (&r)[64]) { for (int i = 0; i < 64; i++) r[i] = orig[i]; });
+      bool same = len2 == len;
+      for (uint32_t i = 0; same && i < (len + 63) / 64; i++) {
+        uint64_t m = (i == len / 64 && (len & 63)) ? ((1ull << (len & 63)) - 1) : ~0ull;
+        same = (slot2[i] & m) == (slot[i] & m);
+      }
+      if (!same)
+        len = 0xffffffffu;  // reported as an encode mismatch below
     }
     bool ok = len == oend;
     for (uint32_t i = 0; ok && i < (len + 63) / 64; i++) {

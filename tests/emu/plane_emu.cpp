@@ -36,7 +36,7 @@ static uint32_t ref_code(std::vector<uint64_t>& w, uint32_t pos0, uint32_t maxbi
   return pos - pos0;
 }
 
-template <int PREC>
+template <int PREC, bool PLIM>
 static int run(std::mt19937_64& rng, int trials)
 {
   uint32_t lut[256];
@@ -62,11 +62,11 @@ static int run(std::mt19937_64& rng, int trials)
     const uint32_t pos0 = 1 + (uint32_t)(rng() % 40);
     const uint32_t budgets[3] = {4096 * 2, 64 + (uint32_t)(rng() % 2000), 1 + (uint32_t)(rng() % 300)};
     for (uint32_t lim_bits : budgets) {
-      uint32_t maxprec = (t % 3 == 0) ? 1 + (uint32_t)(rng() % PREC) : 64;
+      uint32_t maxprec = (PLIM && t % 3 == 0) ? 1 + (uint32_t)(rng() % PREC) : 64;
       std::vector<uint64_t> rw(200, 0), slot(200, 0);
       uint32_t rlen = ref_code(rw, pos0, lim_bits, maxprec, P, PREC);
       OrSlot os{slot.data(), 399};
-      uint32_t end = code_planes<PREC>(os, lut, pos0, pos0 + lim_bits, maxprec, Pl, Ph);
+      uint32_t end = code_planes<PREC, PLIM>(os, lut, pos0, pos0 + lim_bits, maxprec, Pl, Ph);
       bool ok = end - pos0 == rlen;
       uint32_t e = pos0 + rlen;
       for (uint32_t i = 0; ok && i < (e + 63) / 64; i++) {
@@ -74,11 +74,11 @@ static int run(std::mt19937_64& rng, int trials)
         ok = (slot[i] & m) == (rw[i] & m);
       }
       if (!ok && bad++ < 5)
-        printf("PREC %d trial %d kind %d lim %u maxprec %u: len %u vs ref %u\n", PREC, t, kind, lim_bits, maxprec,
+        printf("PREC %d PLIM %d trial %d kind %d lim %u maxprec %u: len %u vs ref %u\n", PREC, PLIM, t, kind, lim_bits, maxprec,
                end - pos0, rlen);
     }
   }
-  printf("planes%d mismatches %d\n", PREC, bad);
+  printf("planes%d plim%d mismatches %d\n", PREC, PLIM, bad);
   return bad;
 }
 
@@ -88,7 +88,7 @@ int main()
   int bad = 0;
   for (int all : {0, 1}) {  // 1: every wave-level branch entered (other lanes need it)
     emu_any_all = all;
-    bad += run<32>(rng, 20000) + run<64>(rng, 10000);
+    bad += run<32, true>(rng, 20000) + run<64, true>(rng, 10000) + run<32, false>(rng, 20000) + run<64, false>(rng, 10000);
   }
   printf("mismatches %d\n", bad);
   return bad != 0;

@@ -8,6 +8,7 @@
 #define __device__
 #define __host__
 #define __global__
+#define __constant__
 #define __shared__ static
 #define __forceinline__ inline
 #define __launch_bounds__(...)
@@ -15,6 +16,7 @@
 // needed the branch: per-lane predication inside such branches is exercised.
 inline bool emu_any_all = false;
 static inline int __any(int x) { return x != 0 || emu_any_all; }
+static inline uint64_t __builtin_amdgcn_ballot_w64(bool x) { return (x || emu_any_all) ? 1u : 0u; }
 static inline int __popc(uint32_t x) { return __builtin_popcount(x); }
 static inline int __popcll(uint64_t x) { return __builtin_popcountll(x); }
 static inline int __clzll(long long x) { return x ? __builtin_clzll((uint64_t)x) : 64; }
@@ -41,7 +43,8 @@ static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t 
 }
 #define __ATOMIC_RELAXED_STUB 0
 #define __HIP_MEMORY_SCOPE_WAVEFRONT 1
-template <typename T> static inline T __hip_atomic_fetch_or(T* p, T v, int, int) { T o = *p; *p |= v; return o; }
+// atomic: the 4-lane emulation (quad_emu.cpp) ORs into one slot from four threads
+template <typename T> static inline T __hip_atomic_fetch_or(T* p, T v, int, int) { return __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
 static inline uint32_t __umulhi(uint32_t a, uint32_t b) { return (uint32_t)(((uint64_t)a * b) >> 32); }
 struct float4 { float x, y, z, w; };
 struct double2 { double x, y; };

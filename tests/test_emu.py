@@ -1,4 +1,4 @@
-"""Host (single-lane) emulation of the device codec against the oracle.
+"""Host emulation of the device codec against the oracle (one lane; one quad for 4D).
 
 The device headers (zfp-par_amd/csrc/hip/{codec_dev,block3}.h) are compiled
 with g++ behind a stub hip_runtime.h (tests/emu/stub) in which a wave is one
@@ -53,3 +53,13 @@ def test_plane_coder_matches_reference_loop(tmp_path):
     r = subprocess.run([_build(str(tmp_path), "plane_emu.cpp")], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "mismatches 0" in r.stdout
+
+
+def test_4d_quad_codec_matches_oracle_all_modes(oracle_obj):
+    """block4.h run as four threads (one quad): DPP permutes and barriers are a
+    four-thread rendezvous, so the quad reductions, the w-lift exchange and the
+    segment-parallel plane coder/decoder are checked bit for bit on the CPU."""
+    d, obj = oracle_obj
+    r = subprocess.run([_build(d, "quad_emu.cpp", [obj, "-pthread"])], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(" 0/200 bad") == 32, r.stdout

@@ -1,0 +1,121 @@
+"""4D parity of the MI355X codec with the oracle (one 4^4 block per quad of lanes).
+
+Same call sequence and bar as test_gpu_codec.py (the reference's end-to-end
+tests, tests/src/endtoend/zfpEndtoendBase.c): zfp_compress / zfp_decompress
+through the C API; streams and decompressed arrays bit-identical to the CPU
+oracle, which test_oracle.py pins to the reference's 4dFloat golden checksums.
+BASELINE C5 (512^4 f32 reversible) runs this path at scale.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from pyoracle import TYPE_DOUBLE, TYPE_FLOAT
+from test_gpu_codec import MODES, _oracle_bytes, _params
+
+pytestmark = pytest.mark.gpu
+
+
+def _field4(shape, dtype, rng):
+    a = (rng.standard_normal(shape) * rng.choice([1e-3, 1.0, 1e5], size=shape)).astype(dtype)
+    flat = a.reshape(-1)
+    info = np.finfo(dtype)
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, info.tiny, info.tiny / 4, -info.tiny / 8,
+                         info.max, -info.max], dtype=dtype)
+    idx = rng.choice(flat.size, size=max(1, flat.size // 50), replace=False)
+    flat[idx] = rng.choice(specials, size=idx.size)
+    if min(shape) >= 8:
+        a[:4, :4, :4, :4] = info.tiny / 16
+        a[4:8, :4, :4, :4] = -0.0
+        a[:4, 4:8, :4, :4] = 0.0
+        a[4:8, 4:8, :4, :4] = np.nan
+    return a
+
+
+def _free_index(product):
+    if product.last_index:
+        product.lib.zfp_hip_index_free(product.last_index)
+        product.last_index = None
+
+
+def test_golden_checksums_4d_float(product, oracle, golden):
+    """The reference's own 4dFloat golden stream + decompressed-array hashes."""
+    field = oracle.smooth_field(4, np.float32)
+    cases = {}
+    for e in golden:
+        if e["dims"] == 4 and e["type"] == "float" and e["subject"] != "input":
+            cases.setdefault((e["mode"], e["param"]), {})[e["subject"]] = int(e["checksum"], 16)
+    assert cases
+    for (mode, param), want in sorted(cases.items(), key=str):
+        data = product.compress(field, mode, param, ztype=3)
+        words = np.frombuffer(data, dtype=np.uint64)
+        assert oracle.hash_words(words) == want["stream"], (mode, param)
+        out, n = product.decompress(data, field.shape, np.float32, mode, param, ztype=3, index=product.last_index)
+        assert n == len(data), (mode, param)
+        if "decompressed" in want:
+            assert oracle.hash_array(out) == want["decompressed"], (mode, param)
+        _free_index(product)
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("shape", [(4, 4, 4, 4), (5, 6, 7, 9), (9, 3, 4, 21), (8, 8, 8, 12)])
+@pytest.mark.parametrize("mode,param", MODES)
+def test_stream_and_roundtrip_match_oracle_4d(product, oracle, dtype, shape, mode, param):
+    rng = np.random.default_rng(zlib.crc32(repr((shape, mode, param, np.dtype(dtype).name, 4)).encode()))
+    a = _field4(shape, dtype, rng)
+    ztype = TYPE_FLOAT if dtype == np.float32 else TYPE_DOUBLE
+    want, end = _oracle_bytes(oracle, a, mode, param)
+    got = product.compress(a, mode, param, ztype=ztype)
+    assert got == want
+    params = _params(mode, param, ztype, a.ndim)
+    ref_out, _ = oracle.decompress_words(np.frombuffer(want, dtype=np.uint64), a.shape, dtype, params)
+    out, n = product.decompress(got, a.shape, dtype, mode, param, ztype=ztype, index=product.last_index)
+    assert n == len(got)
+    assert out.tobytes() == ref_out.tobytes()
+    _free_index(product)
+
+
+@pytest.mark.parametrize("mode,param", [("rate", 8), ("rate", 3.25), ("reversible", None)])
+def test_header_offset_stream_matches_oracle_4d(product, oracle, mode, param):
+    """zfpy's 96-bit header first: 4D blocks start at bit 96."""
+    rng = np.random.default_rng(13)
+    a = rng.standard_normal((6, 8, 9, 10)).astype(np.float32)
+    got = product.compress(a, mode, param, ztype=0, header=True)
+    words = np.frombuffer(got + bytes((-len(got)) % 8), dtype=np.uint64).copy()
+    params = _params(mode, param, 0, 4)
+    ow, end = oracle.compress_words(a, params, bit_offset=96)
+    payload = words.copy()
+    payload[0] = 0
+    payload[1] &= ~np.uint64((1 << 32) - 1)
+    assert payload[: len(ow)].tobytes() == ow.tobytes()
+    assert len(got) == (end + 63) // 64 * 8
+    out, _ = product.decompress(got, a.shape, np.float32, mode, param, ztype=0, header=True,
+                                index=product.last_index)
+    ref, _ = oracle.decompress_words(ow, a.shape, np.float32, params, bit_offset=96)
+    assert out.tobytes() == ref.tobytes()
+    _free_index(product)
+
+
+@pytest.mark.parametrize("box", [[(0, 8), (4, 12), (0, 9), (4, 8)], [(4, 13), (0, 8), (4, 9), (0, 6)]])
+@pytest.mark.parametrize("mode,param", [("rate", 8), ("precision", 16), ("reversible", None)])
+def test_chunk_boxes_match_oracle_4d(product, oracle, box, mode, param):
+    """zfp_compress_chunk over a 4D sub-box, strided field as zfpy builds it."""
+    rng = np.random.default_rng(7)
+    a = rng.standard_normal((8, 9, 12, 13)).astype(np.float32)
+    got = product.compress(a, mode, param, ztype=3, chunk=box, strided=True)
+    want, end = _oracle_bytes(oracle, a, mode, param, ztype=3, box=box)
+    assert got == want
+    _free_index(product)
+
+
+def test_reversible_lossless_4d(product, oracle):
+    """C5's mode on the reference's smooth 4D field: lossless and bit-exact."""
+    a = oracle.smooth_field(4, np.float32)
+    got = product.compress(a, "reversible", None, ztype=3)
+    want, _ = _oracle_bytes(oracle, a, "reversible", None)
+    assert got == want
+    out, n = product.decompress(got, a.shape, np.float32, "reversible", None, ztype=3, index=product.last_index)
+    assert n == len(got)
+    assert out.tobytes() == a.tobytes()
+    _free_index(product)

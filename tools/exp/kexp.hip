@@ -11,8 +11,11 @@ using namespace zfp_amd;
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 // MODE 0: full; 1: no coder (planes folded into one word); 2: coder on synthetic planes; 3: load+max only
+#ifndef KEXP_WPS
+#define KEXP_WPS 4
+#endif
 template <int MODE>
-__global__ __launch_bounds__(256, 4) void enc_var(const float* __restrict__ data, Geometry g, CodecParams cp,
+__global__ __launch_bounds__(256, KEXP_WPS) void enc_var(const float* __restrict__ data, Geometry g, CodecParams cp,
                                                  uint64_t* __restrict__ out, uint32_t sw, uint32_t swp, uint32_t magic)
 {
   __shared__ uint32_t lut[256];
@@ -36,13 +39,13 @@ __global__ __launch_bounds__(256, 4) void enc_var(const float* __restrict__ data
         Pl[k] = h & keep;
         Ph[k] = (h * 7u) & (k > 12 ? 0u : ~0u);
       }
-      code_planes<32>(os, lut, 9, cp.maxbits, 32, Pl, Ph);
+      code_planes<32, false>(os, lut, 9, cp.maxbits, 32, Pl, Ph);
     } else {
       float v[64];
       BlockPos p = block_pos(g, b, 3);
       gather3<float, true>(v, data, g, p);
       if (MODE == 0) {
-        encode_block3<float, false>(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+        encode_block3<float, false, true>(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
       } else if (MODE == 1) {
         int32_t q[64];
         uint32_t mp;

@@ -157,27 +157,31 @@ __device__ __forceinline__ void scatter3(const S (&v)[64], S* __restrict__ base,
 
 // ---- coefficient order + negabinary, then bit planes ----
 // Planes as two 32-bit halves: Pl[k] bit i = plane k of coefficient i (i < 32),
-// Ph[k] bit i = plane k of coefficient 32 + i.
+// Ph[k] bit i = plane k of coefficient 32 + i.  P3: q is in raster order and is
+// read through kPerm3 (3D); false: q is already in coding order (a 4D lane's
+// segment, block4.h).
+template <bool P3 = true>
 __device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[32], uint32_t (&Ph)[32], const int32_t (&q)[64])
 {
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    Pl[i] = ((uint32_t)q[kPerm3[i]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
-    Ph[i] = ((uint32_t)q[kPerm3[i + 32]] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    Pl[i] = ((uint32_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    Ph[i] = ((uint32_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
   }
   transpose32(Pl);
   transpose32(Ph);
 }
 
 // double: planes 32..63 from the high words; 0..31 only when `need_low`
+template <bool P3 = true>
 __device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[64], uint32_t (&Ph)[64], const int64_t (&q)[64],
                                                    bool need_low)
 {
   uint32_t a[32], b[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    uint64_t u0 = ((uint64_t)q[kPerm3[i]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
-    uint64_t u1 = ((uint64_t)q[kPerm3[i + 32]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    uint64_t u0 = ((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    uint64_t u1 = ((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
     a[i] = (uint32_t)(u0 >> 32);
     b[i] = (uint32_t)(u1 >> 32);
   }
@@ -191,8 +195,8 @@ __device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[64], uint32_t 
   if (__any(need_low)) {
 #pragma unroll
     for (int i = 0; i < 32; i++) {
-      uint64_t u0 = ((uint64_t)q[kPerm3[i]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
-      uint64_t u1 = ((uint64_t)q[kPerm3[i + 32]] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+      uint64_t u0 = ((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+      uint64_t u1 = ((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
       a[i] = (uint32_t)u0;
       b[i] = (uint32_t)u1;
     }
@@ -212,6 +216,7 @@ __device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[64], uint32_t 
   }
 }
 
+template <bool P3 = true>
 __device__ __forceinline__ void coeffs_from_planes(int32_t (&q)[64], const uint64_t (&P)[32])
 {
   uint32_t lo[32], hi[32];
@@ -224,11 +229,12 @@ __device__ __forceinline__ void coeffs_from_planes(int32_t (&q)[64], const uint6
   transpose32(hi);
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    q[kPerm3[i]] = (int32_t)((lo[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
-    q[kPerm3[i + 32]] = (int32_t)((hi[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+    q[P3 ? kPerm3[i] : i] = (int32_t)((lo[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+    q[P3 ? kPerm3[i + 32] : i + 32] = (int32_t)((hi[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
   }
 }
 
+template <bool P3 = true>
 __device__ __forceinline__ void coeffs_from_planes(int64_t (&q)[64], const uint64_t (&P)[64], bool need_low)
 {
   uint32_t a[32], b[32], c[32], d[32];
@@ -258,8 +264,8 @@ __device__ __forceinline__ void coeffs_from_planes(int64_t (&q)[64], const uint6
   for (int i = 0; i < 32; i++) {
     uint64_t u0 = ((uint64_t)a[i] << 32) | c[i];
     uint64_t u1 = ((uint64_t)b[i] << 32) | d[i];
-    q[kPerm3[i]] = (int64_t)((u0 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
-    q[kPerm3[i + 32]] = (int64_t)((u1 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+    q[P3 ? kPerm3[i] : i] = (int64_t)((u0 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+    q[P3 ? kPerm3[i + 32] : i + 32] = (int64_t)((u1 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
   }
 }
 
@@ -272,7 +278,7 @@ __device__ __forceinline__ uint32_t precision3(int emax, const CodecParams& cp)
 
 // integer part of the block: order, planes, coder (encode.c:260-280).
 // Codes from bit `pos` of the slot; returns the end position (<= lim).
-template <typename Int>
+template <bool PLIM, typename Int>
 __device__ __forceinline__ uint32_t encode_ints3(OrSlot& w, const uint32_t* lut, Int (&q)[64], uint32_t pos,
                                                  uint32_t lim, uint32_t prec)
 {
@@ -283,7 +289,7 @@ __device__ __forceinline__ uint32_t encode_ints3(OrSlot& w, const uint32_t* lut,
     planes_from_coeffs(Pl, Ph, q);
   else
     planes_from_coeffs(Pl, Ph, q, prec > 32);
-  return code_planes<PREC>(w, lut, pos, lim, prec, Pl, Ph);
+  return code_planes<PREC, PLIM>(w, lut, pos, lim, prec, Pl, Ph);
 }
 
 template <typename Int>
@@ -352,8 +358,9 @@ __device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], double (&v)[64]
 }
 
 // Encode one block into a zeroed slot; returns its length in bits including
-// minbits padding (padding bits are the slot's zeros).
-template <typename S, bool REV, typename Reload>
+// minbits padding (padding bits are the slot's zeros).  FR: fixed rate with
+// maxprec >= intprec (no per-block precision limit; see code_planes).
+template <typename S, bool REV, bool FR = false, typename Reload>
 __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut, S (&v)[64], const CodecParams& cp,
                                                   Reload&& reload)
 {
@@ -410,7 +417,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
     if (prec > cp.maxprec) prec = cp.maxprec;
     if (prec < 1) prec = 1;
     w.put32(bits, prec - 1);
-    const uint32_t end = encode_ints3(w, lut, q, bits + T::kPbits, cp.maxbits, prec);
+    const uint32_t end = encode_ints3<true>(w, lut, q, bits + T::kPbits, cp.maxbits, prec);
     uint32_t ib = end - bits;
     if (ib < minb) ib = minb;
     return bits + ib;
@@ -425,7 +432,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
       bits += kE;
       xform<3, false, false>(q);
       const uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
-      uint32_t ib = encode_ints3(w, lut, q, bits, cp.maxbits, mp) - bits;
+      uint32_t ib = encode_ints3<!FR>(w, lut, q, bits, cp.maxbits, mp) - bits;
       if (ib < minb) ib = minb;
       bits += ib;
     } else if (cp.minbits > bits) {

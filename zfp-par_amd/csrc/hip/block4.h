@@ -1,0 +1,569 @@
+// Per-quad codec of one 4x4x4x4 block (float or double) for every zfp mode.
+//
+// The four lanes of a quad (lanes 4q .. 4q+3, 16 blocks per wave) share a
+// block.  Lane r holds
+//   * up to the w-lift: the 3D slice w = r (64 values, raster x + 4y + 16z),
+//     so gather, block-floating-point cast and the x, y, z lifts are the 3D
+//     per-lane code (block3.h);
+//   * after the w-lift and the reordering: the coefficients of coding order
+//     64r .. 64r+63 (codec4.c perm_4), i.e. bits [64r, 64r+64) of every
+//     256-bit bit plane -- the 3D plane representation (Pl/Ph halves), per lane.
+// The w-lift and the reordering go through a per-block LDS exchange area.
+// Block-wide values (max, OR, prefix sums over the four plane segments) are
+// quad reductions on DPP quad permutes, so every branch on them is
+// quad-uniform.
+//
+// encode_block4: encodef.c:63-90, revencodef.c:45-80, encode.c:136-175 and
+//                208-234 (encode_many_ints[_prec]), transform encode4.c:40-65,
+//                gather/pad encode4.c:4-38.
+// decode_block4: decodef.c:7-36, revdecodef.c:22-59, decode.c:122-173 and
+//                212-246, inverse transform decode4.c:27-52.
+#pragma once
+
+#include "block3.h"
+
+namespace zfp_amd {
+
+// ---------------------------------------------------------------------------
+// quad permutes: DPP quad_perm, lane i of each quad reads lane sel_i
+// (ctrl = sel_0 | sel_1 << 2 | sel_2 << 4 | sel_3 << 6).  Called only where the
+// whole quad is active.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t x)
+{
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t qperm(uint64_t x)
+{
+  return ((uint64_t)qperm<CTRL>((uint32_t)(x >> 32)) << 32) | qperm<CTRL>((uint32_t)x);
+}
+
+constexpr int kQSwap1 = 0xb1;  // [1,0,3,2]
+constexpr int kQSwap2 = 0x4e;  // [2,3,0,1]
+
+template <typename U>
+__device__ __forceinline__ U quad_max(U x)
+{
+  U y = qperm<kQSwap1>(x);
+  x = x > y ? x : y;
+  y = qperm<kQSwap2>(x);
+  return x > y ? x : y;
+}
+
+template <typename U>
+__device__ __forceinline__ U quad_or(U x)
+{
+  x |= qperm<kQSwap1>(x);
+  return x | qperm<kQSwap2>(x);
+}
+
+// exclusive prefix sum over the quad; `total` receives the quad's sum
+__device__ __forceinline__ uint32_t quad_excl(uint32_t x, uint32_t& total)
+{
+  const uint32_t r = threadIdx.x & 3u;
+  const uint32_t x1 = qperm<0x90>(x);  // [0,0,1,2]: lane r - 1
+  const uint32_t a = x + (r >= 1u ? x1 : 0u);
+  const uint32_t a2 = qperm<0x40>(a);  // [0,0,0,1]: lane r - 2
+  const uint32_t s = a + (r >= 2u ? a2 : 0u);
+  total = qperm<0xff>(s);  // lane 3
+  return s - x;
+}
+
+// block max |x| (NaN ignored) over the quad's four slices
+template <typename S>
+__device__ __forceinline__ S quad_absmax(const S (&v)[64])
+{
+  const S m = block_absmax(v);  // >= +0, never NaN: ordered like its bit pattern
+  if constexpr (sizeof(S) == 4)
+    return __uint_as_float(quad_max(__float_as_uint(m)));
+  else
+    return __longlong_as_double((long long)quad_max((uint64_t)__double_as_longlong(m)));
+}
+
+// ---------------------------------------------------------------------------
+// Gather / scatter of lane r's slice.  A partial block is padded along w by
+// reading the slice the pad rule copies (encode.c:9-27: nw = 1 -> all from
+// w = 0; nw = 2 -> w2 = w1, w3 = w0; nw = 3 -> w3 = w0); x, y, z padding is the
+// 3D gather's.
+__device__ __forceinline__ int pad_src_w(int r, int nw)
+{
+  return r < nw ? r : ((r == 2 && nw == 2) ? 1 : 0);
+}
+
+__device__ __forceinline__ BlockPos slice_pos(const Geometry& g, const BlockPos& p, int w)
+{
+  BlockPos s = p;
+  s.off = p.off + (int64_t)w * g.s[3];
+  s.full = p.cnt[0] == 4 && p.cnt[1] == 4 && p.cnt[2] == 4;
+  return s;
+}
+
+// ---------------------------------------------------------------------------
+// Exchange area of a block: entry 4 pos + w holds value (pos, w), pos =
+// x + 4y + 16z.  Blocks are kXStride entries apart: 260 = 4 (mod 64), so the 64
+// lanes' slice writes of one pos hit 64 distinct banks (float).
+constexpr uint32_t kXStride = 260;
+
+// Order table: dword k packs the exchange entries of coding-order indices
+// 4k .. 4k+3, one byte each (perm_4 of codec4.c via kPerm4).
+struct OrderTab4 {
+  uint32_t t[64];
+};
+
+constexpr OrderTab4 make_order_tab4()
+{
+  OrderTab4 o{};
+  for (int k = 0; k < 64; k++) {
+    uint32_t t = 0;
+    for (int i = 0; i < 4; i++) {
+      const uint32_t c = kPerm4[4 * k + i];
+      t |= ((c & 63u) * 4u + (c >> 6)) << (8 * i);
+    }
+    o.t[k] = t;
+  }
+  return o;
+}
+
+__constant__ OrderTab4 kOrderTab4 = make_order_tab4();
+
+// forward: slices (after the x, y, z lifts) -> w-lift (encode4.c:60-64) ->
+// lane r gets the coefficients of coding order 64r .. 64r+63.  Called by the
+// whole wave (one 64-thread workgroup).
+template <bool REV, typename Int>
+__device__ __forceinline__ void exchange_fwd(Int (&q)[64], Int* X, const uint32_t* tab)
+{
+  const uint32_t r = threadIdx.x & 3u;
+#pragma unroll
+  for (int i = 0; i < 64; i++)
+    X[4 * i + r] = q[i];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    Int* e = X + 4 * (16 * r + j);
+    Int a = e[0], b = e[1], c = e[2], d = e[3];
+    if (REV) Lift<Int>::rfwd(a, b, c, d);
+    else Lift<Int>::fwd(a, b, c, d);
+    e[0] = a;
+    e[1] = b;
+    e[2] = c;
+    e[3] = d;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 16; m++) {
+    const uint32_t t = tab[16 * r + m];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      q[4 * m + i] = X[(t >> (8 * i)) & 0xffu];
+  }
+  __syncthreads();
+}
+
+// inverse: coefficients in coding order -> inverse w-lift (decode4.c:31-36) ->
+// lane r gets slice w = r
+template <bool REV, typename Int>
+__device__ __forceinline__ void exchange_inv(Int (&q)[64], Int* X, const uint32_t* tab)
+{
+  const uint32_t r = threadIdx.x & 3u;
+  __syncthreads();
+#pragma unroll
+  for (int m = 0; m < 16; m++) {
+    const uint32_t t = tab[16 * r + m];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+      X[(t >> (8 * i)) & 0xffu] = q[4 * m + i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; j++) {
+    Int* e = X + 4 * (16 * r + j);
+    Int a = e[0], b = e[1], c = e[2], d = e[3];
+    if (REV) Lift<Int>::rinv(a, b, c, d);
+    else Lift<Int>::inv(a, b, c, d);
+    e[0] = a;
+    e[1] = b;
+    e[2] = c;
+    e[3] = d;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 64; i++)
+    q[i] = X[4 * i + r];
+}
+
+// zero `words` 64-bit words at w (whole wave)
+__device__ __forceinline__ void zero_region(uint64_t* w, uint32_t words)
+{
+  for (uint32_t i = threadIdx.x & 63u; i < words; i += 64)
+    w[i] = 0;
+  __syncthreads();
+}
+
+// ---------------------------------------------------------------------------
+// Embedded coder over 256-coefficient planes (encode.c:136-175, 208-234).
+// Same closed form as code_planes (codec_dev.h) with the plane split into four
+// 64-bit segments: lane r writes its segment's verbatim bits at pos + 64r and
+// the doubled-ones expansion of its part of xs at the offset given by the
+// quad's exclusive scan of the new ones below it; the lane holding the top
+// one removes the top pair's surplus.  Every slot write is clamped per dword
+// to the slot's last dword (jmax, past the budget), so bits beyond the budget
+// never touch a dword that holds block bits.
+__device__ __forceinline__ void or64_clamped(uint32_t* d, uint32_t jmax, uint32_t p, uint32_t v0, uint32_t v1)
+{
+  const uint32_t j = (p + 31u) >> 5;  // p >= 1: dwords j-1 .. j+1
+  const uint32_t t = 0u - p;
+  lds_or32(d + min(j - 1u, jmax), __builtin_amdgcn_alignbit(v0, 0u, t));
+  lds_or32(d + min(j, jmax), __builtin_amdgcn_alignbit(v1, v0, t));
+  lds_or32(d + min(j + 1u, jmax), __builtin_amdgcn_alignbit(0u, v1, t));
+}
+
+// doubled-ones expansion of 32 bits (32 + popcount bits <= 64)
+__device__ __forceinline__ uint64_t dbl32(const uint32_t* lut, uint32_t x)
+{
+  const uint32_t lo = x & 0xffffu;
+  return (uint64_t)dbl16(lut, lo) | ((uint64_t)dbl16(lut, x >> 16) << (16u + (uint32_t)__popc(lo)));
+}
+
+template <int PREC>
+__device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, const uint32_t* lut, uint32_t pos,
+                                                 uint32_t lim, uint32_t maxprec, const uint32_t (&Pl)[PREC],
+                                                 const uint32_t (&Ph)[PREC])
+{
+  const uint32_t r = threadIdx.x & 3u;
+  const uint32_t base = 64u * r;  // first coefficient of this lane's segment
+  const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
+  uint32_t p = pos, n = 0;
+#pragma unroll
+  for (int k = PREC - 1; k >= 0; k--) {
+    const bool act = p < lim && (uint32_t)k >= kmin;  // quad-uniform
+    if (__builtin_amdgcn_ballot_w64(act) == 0)
+      break;
+    const uint64_t P = ((uint64_t)Ph[k] << 32) | Pl[k];
+    const uint32_t nr = n > base ? min(n - base, 64u) : 0u;  // significant coefficients of the segment
+    const uint64_t S = low_mask(nr);
+    const uint64_t N = P & ~S;
+    const uint32_t bl = N ? 64u - (uint32_t)__clzll((long long)N) : 0u;
+    const uint32_t top1 = quad_max(bl ? base + bl : 0u);  // 1 + top new one of the plane (0: none)
+    const uint32_t c = (uint32_t)__popcll(N);
+    uint32_t ctot;
+    const uint32_t cex = quad_excl(c, ctot);
+    const uint32_t n1 = top1 ? top1 : n;
+    const uint32_t impl = top1 == 256u ? 1u : 0u;  // coefficient 255: its one and test are implicit
+    const uint32_t dlen = n1 + ctot + 1u - (n1 == 256u ? 1u : 0u) - impl;
+    if (act) {
+      const uint64_t V = P & S;
+      if (nr)
+        or64_clamped(d, jmax, p + base, (uint32_t)V, (uint32_t)(V >> 32));
+      if (top1 && r == 0u) {  // the plane's positive group test
+        const uint32_t gp = p + n;
+        lds_or32(d + min(gp >> 5, jmax), 1u << (gp & 31u));
+      }
+      const uint64_t xs = nr < 64u ? N >> nr : 0ull;
+      if (xs) {
+        const uint32_t x0 = (uint32_t)xs, x1 = (uint32_t)(xs >> 32);
+        uint64_t E0 = dbl32(lut, x0), E1 = dbl32(lut, x1);
+        const uint32_t L0 = 32u + (uint32_t)__popc(x0);
+        if (base + bl == top1) {
+          // top one at xs bit h; its pair starts at h + (c - 1) of the expansion
+          const uint32_t h = bl - 1u - nr;
+          const uint32_t t = h + c - 1u;
+          if (h < 32u)
+            E0 &= ~((uint64_t)(2u | impl) << t);
+          else
+            E1 &= ~((uint64_t)(2u | impl) << (t - L0));
+        }
+        const uint32_t co = p + 1u + base + nr + cex;
+        or64_clamped(d, jmax, co, (uint32_t)E0, (uint32_t)(E0 >> 32));
+        if (x1)
+          or64_clamped(d, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
+      }
+    }
+    p = act ? p + dlen : p;
+    n = act ? n1 : n;
+  }
+  return p < lim ? p : lim;
+}
+
+// Decoder twin (decode.c:122-173, 212-246): the quad parses the group tests
+// redundantly (same stream bits, same control flow), each lane keeping the
+// ones of its segment; verbatim bits are read per segment.  One iteration per
+// group test, i.e. per newly significant coefficient plus one per plane.
+template <int PREC>
+__device__ __forceinline__ uint32_t decode_planes4(WordReader& rd, uint32_t budget, uint32_t maxprec,
+                                                   uint64_t (&P)[PREC])
+{
+  const uint32_t r = threadIdx.x & 3u;
+  const uint32_t base = 64u * r;
+  const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
+  uint32_t bits = budget, n = 0;
+#pragma unroll
+  for (int k = 0; k < PREC; k++)
+    P[k] = 0;
+#pragma unroll
+  for (int k = PREC - 1; k >= 0; k--) {
+    const bool act = bits != 0 && (uint32_t)k >= kmin;
+    if (__builtin_amdgcn_ballot_w64(act) == 0)
+      break;
+    if (act) {
+      const uint32_t m = n < bits ? n : bits;
+      const uint32_t cnt = m > base ? min(m - base, 64u) : 0u;
+      WordReader seg{rd.w, rd.pos + base};
+      uint64_t x = seg.read(cnt);
+      rd.skip(m);
+      bits -= m;
+      while (n < 256u && bits) {
+        bits--;
+        if (!rd.read1())
+          break;
+        for (;;) {  // zeros up to the next one, at most to coefficient 255 / the budget
+          const uint32_t lim = min(255u - n, bits);
+          const uint32_t z = ctz64(rd.peek64());  // 64: no one in the next 64 bits
+          if (z >= lim) {
+            rd.skip(lim);
+            bits -= lim;
+            n += lim;
+            break;
+          }
+          if (z < 64u) {
+            rd.skip(z + 1);
+            bits -= z + 1;
+            n += z;
+            break;
+          }
+          rd.skip(64);
+          bits -= 64;
+          n += 64;
+        }
+        if (n - base < 64u)
+          x |= 1ull << (n - base);
+        n++;
+      }
+      P[k] = x;
+    }
+  }
+  return budget - bits;
+}
+
+__device__ __forceinline__ uint32_t precision4(int emax, const CodecParams& cp)
+{
+  int p = emax - cp.minexp + 2 * (4 + 1);
+  if (p < 0) p = 0;
+  return (uint32_t)p < cp.maxprec ? (uint32_t)p : cp.maxprec;
+}
+
+// lossy exponent + cast (the 3D fast path with quad-wide maxima)
+template <typename Reload>
+__device__ __forceinline__ int lossy_emax_cast4(int32_t (&q)[64], float (&v)[64], const CodecParams& cp,
+                                                uint32_t& mp, Reload&& reload)
+{
+  int32_t mi = 0;
+  uint32_t mu = 0;
+#pragma unroll
+  for (int i = 0; i < 64; i++) {
+    const uint32_t b = __float_as_uint(v[i]);
+    mi = max(mi, (int32_t)b);
+    mu = max(mu, b);
+  }
+  const uint32_t mb = quad_max(max((uint32_t)mi, mu & 0x7fffffffu));
+  int emax = mb == 0 ? -127 : ((mb >> 23) == 0 ? -126 : (int)(mb >> 23) - 126);
+  const bool bad = mb >= 0x7f800000u;  // inf/NaN in the block: NaN-ignoring max
+  if (__any(bad)) {
+    const float am = quad_absmax(v);
+    if (bad)
+      emax = block_emax(am);
+  }
+  mp = precision4(emax, cp);
+  const bool cast = mp != 0 && emax != -127;
+  const float s = __uint_as_float((uint32_t)(157 - emax) << 23);
+#pragma unroll
+  for (int i = 0; i < 64; i++)
+    q[i] = (int32_t)(s * v[i]);
+  if (__any(cast && (bad || emax < -97))) {
+    float w[64];
+    reload(w);
+    fwd_cast(q, w, emax);
+  }
+  return emax;
+}
+
+template <typename Reload>
+__device__ __forceinline__ int lossy_emax_cast4(int64_t (&q)[64], double (&v)[64], const CodecParams& cp,
+                                                uint32_t& mp, Reload&&)
+{
+  const int emax = block_emax(quad_absmax(v));
+  mp = precision4(emax, cp);
+  fwd_cast(q, v, emax);
+  return emax;
+}
+
+// Encode the quad's block into its zeroed slot (d: dwords, jmax: last dword);
+// returns the block length in bits including minbits padding.  Called by the
+// whole wave: the exchange and the slot zeroing are wave-wide (`region`,
+// `region_words`: the wave's slot area, which aliases the exchange areas).
+template <typename S, bool REV, typename Reload>
+__device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, const uint32_t* lut, const uint32_t* tab,
+                                                  typename Traits<S>::Int* X, uint64_t* region, uint32_t region_words,
+                                                  S (&v)[64], const CodecParams& cp, Reload&& reload)
+{
+  using T = Traits<S>;
+  using Int = typename T::Int;
+  using UInt = typename T::UInt;
+  constexpr uint32_t kE = T::kEbits;
+  constexpr int PREC = T::kIntPrec;
+  const uint32_t r = threadIdx.x & 3u;
+  OrSlot os{reinterpret_cast<uint64_t*>(d), jmax};
+  Int q[64];
+  uint32_t Pl[PREC], Ph[PREC];
+  if constexpr (REV) {
+    // reversible (revencodef.c:45-80)
+    const int emax = block_emax(quad_absmax(v));
+    bool same = true;
+    if (emax != -T::kEbias) {
+      fwd_cast(q, v, emax);
+      const S s = (sizeof(S) == 4) ? (S)pow2f(emax - 30) : (S)pow2d(emax - 62);
+#pragma unroll
+      for (int i = 0; i < 64; i++)
+        same = same && (bits_of((S)(s * (S)q[i])) == bits_of(v[i]));
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; i++) {
+        q[i] = 0;
+        same = same && (bits_of(v[i]) == 0);
+      }
+    }
+    same = quad_or(same ? 0u : 1u) == 0u;
+    if (!same) {
+#pragma unroll
+      for (int i = 0; i < 64; i++) {
+        const Int x = (Int)bits_of(v[i]);
+        q[i] = x < 0 ? (Int)((UInt)x ^ T::kTcMask) : x;
+      }
+    }
+    xform<3, false, true>(q);
+    exchange_fwd<true>(q, X, tab);
+    zero_region(region, region_words);
+    const uint32_t e = (uint32_t)(emax + T::kEbias);
+    if (same && !e)
+      return 1u < cp.minbits ? cp.minbits : 1u;  // a single 0 bit
+    uint32_t bits;
+    if (same) {
+      if (r == 0u) os.head(1u | (e << 2));
+      bits = 2 + kE;
+    } else {
+      if (r == 0u) os.head(3u);
+      bits = 2;
+    }
+    // rev_encode_block (revencode.c:54-76): precision from the OR of all 256
+    const uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
+    UInt all = 0;
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      all |= ((UInt)q[i] + T::kNbMask) ^ T::kNbMask;
+    all = quad_or(all);
+    uint32_t prec = all ? (uint32_t)(PREC - (sizeof(S) == 4 ? __builtin_ctz((uint32_t)all)
+                                                            : __builtin_ctzll((uint64_t)all)))
+                        : 0u;
+    if (prec > cp.maxprec) prec = cp.maxprec;
+    if (prec < 1) prec = 1;
+    if (r == 0u) os.put32(bits, prec - 1);
+    if constexpr (PREC == 32)
+      planes_from_coeffs<false>(Pl, Ph, q);
+    else
+      planes_from_coeffs<false>(Pl, Ph, q, prec > 32);
+    const uint32_t end = code_planes4<PREC>(d, jmax, lut, bits + T::kPbits, cp.maxbits, prec, Pl, Ph);
+    uint32_t ib = end - bits;
+    if (ib < minb) ib = minb;
+    return bits + ib;
+  } else {
+    // lossy (encodef.c:63-90)
+    uint32_t mp;
+    const int emax = lossy_emax_cast4(q, v, cp, mp, reload);
+    const uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
+    xform<3, false, false>(q);
+    exchange_fwd<false>(q, X, tab);
+    zero_region(region, region_words);
+    uint32_t bits = 1;
+    if (e) {
+      if (r == 0u) os.head(2 * e + 1);
+      bits += kE;
+      const uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
+      if constexpr (PREC == 32)
+        planes_from_coeffs<false>(Pl, Ph, q);
+      else
+        planes_from_coeffs<false>(Pl, Ph, q, mp > 32);
+      uint32_t ib = code_planes4<PREC>(d, jmax, lut, bits, cp.maxbits, mp, Pl, Ph) - bits;
+      if (ib < minb) ib = minb;
+      bits += ib;
+    } else if (cp.minbits > bits) {
+      bits = cp.minbits;
+    }
+    return bits;
+  }
+}
+
+// Decode the quad's block (invalid quads decode nothing but take part in the
+// wave-wide exchange); lane r receives slice w = r.
+template <typename S, bool REV>
+__device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const CodecParams& cp,
+                                              typename Traits<S>::Int* X, const uint32_t* tab, bool valid)
+{
+  using T = Traits<S>;
+  using Int = typename T::Int;
+  using UInt = typename T::UInt;
+  constexpr uint32_t kE = T::kEbits;
+  constexpr int PREC = T::kIntPrec;
+  Int q[64];
+#pragma unroll
+  for (int i = 0; i < 64; i++)
+    q[i] = 0;
+  int emax = 0;
+  uint32_t kind = 0;  // 0: zero block, 1: block-floating-point, 2: reinterpreted bits
+  if (valid && rd.read1()) {
+    uint32_t bits = 1;
+    uint32_t prec;
+    if constexpr (REV) {
+      bits++;
+      const bool reinterp = rd.read1() != 0;
+      if (!reinterp) {
+        bits += kE;
+        emax = (int)rd.read(kE) - T::kEbias;
+      }
+      prec = (uint32_t)rd.read(T::kPbits) + 1;
+      bits += T::kPbits;
+      kind = reinterp ? 2u : (emax != -T::kEbias ? 1u : 0u);
+    } else {
+      bits += kE;
+      emax = (int)rd.read(kE) - T::kEbias;
+      prec = precision4(emax, cp);
+      kind = 1;
+    }
+    uint64_t P[PREC];
+    decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+    if constexpr (PREC == 32)
+      coeffs_from_planes<false>(q, P);
+    else
+      coeffs_from_planes<false>(q, P, prec > 32);
+  }
+  exchange_inv<REV>(q, X, tab);
+  xform<3, true, REV>(q);
+  if (REV && kind == 2u) {
+#pragma unroll
+    for (int i = 0; i < 64; i++) {
+      const Int x = q[i] < 0 ? (Int)((UInt)q[i] ^ T::kTcMask) : q[i];
+      if constexpr (sizeof(S) == 4)
+        v[i] = __uint_as_float((uint32_t)x);
+      else
+        v[i] = __longlong_as_double((long long)x);
+    }
+  } else if (kind == 1u) {
+    inv_cast(v, q, emax);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      v[i] = 0;
+  }
+}
+
+}  // namespace zfp_amd

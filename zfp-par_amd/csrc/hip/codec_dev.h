@@ -130,9 +130,9 @@ struct OrSlot {
 };
 
 // Slot size (64-bit words) for a block budget of `lim` bits: a plane that starts
-// before lim writes its verbatim bits through dword ceil((lim-1)/32)+1 and its
-// group bits through dword ceil((lim+63)/32); group extensions are clamped.
-__host__ __device__ constexpr uint32_t slot_words_for(uint32_t lim) { return ((lim + 63u + 31u) / 32u) / 2u + 1u; }
+// at or before lim writes its verbatim bits through dword ceil(lim/32)+1 and its
+// group bits through dword ceil((lim+64)/32); group extensions are clamped.
+__host__ __device__ constexpr uint32_t slot_words_for(uint32_t lim) { return ((lim + 95u) / 32u) / 2u + 1u; }
 
 // Doubled-ones table: entry b holds the 8 bits of b LSB first with every one
 // written twice ("1" -> "11", "0" -> "0"), 8 + popcount(b) bits.  The group
@@ -454,78 +454,137 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32])
 // budget is not checked inside a plane: bits beyond it fall past the block end
 // into the slot's spare words.
 //
+// Group units 1..3 of a plane whose top one lies past bit 15 of xs (h >= 16):
+// at most three such planes per block (each makes >= 17 coefficients
+// significant).  The coder records them and expands them after the plane loop.
+struct ExtEvent {
+  uint32_t gp;      // slot position of the plane's group bits
+  uint32_t xl, xh;  // xs
+  uint32_t hb;      // h | implicit << 6 | (bit 32 of g) << 7; h < 16: no event
+};
+
+__device__ __forceinline__ void expand_event(OrSlot& s, const uint32_t* lut, const ExtEvent& e)
+{
+  const uint32_t h = e.hb & 63u, impl = (e.hb >> 6) & 1u;
+  const uint64_t xs = ((uint64_t)e.xh << 32) | e.xl;
+  uint32_t D = 16u + (uint32_t)__popc(e.xl & 0xffffu);  // dbl length of unit 0
+#pragma unroll
+  for (int j = 1; j < 4; j++) {
+    // the branch is entered for the wave: every per-lane effect is predicated
+    const bool unit = h >= 16u * j;
+    if (__any(unit)) {
+      const uint32_t u = (uint32_t)(xs >> (16 * j)) & 0xffffu;
+      const uint32_t cu = (uint32_t)__popc(u);
+      uint32_t dj = dbl16(lut, u);
+      if (h < 16u * (j + 1))  // the top one is in this unit
+        dj -= (2u + impl) << ((h - 16u * j + cu - 1u) & 31u);
+      if (unit) {
+        if (j == 1)  // also carries bit 32 of g (unit 0 all ones)
+          s.put64_clamped(e.gp + D, (dj << 1) | (e.hb >> 7), dj >> 31);
+        else
+          s.put32_clamped(e.gp + 1u + D, dj);
+      }
+      D += 16u + cu;
+    }
+  }
+}
+
 // Codes planes PREC-1 .. PREC-maxprec starting at bit `pos` (>= 1) of the slot;
-// returns the end position clamped to `lim` (the block's bit budget end).  The
-// plane index is wave-uniform, so Pl[k]/Ph[k] are register reads with a scalar
-// index.
-template <int PREC>
+// returns the end position clamped to `lim` (the block's bit budget end).
+// Fully unrolled: plane k is a register, the coder state is renamed, not
+// copied.  PLIM = false (fixed rate, maxprec >= PREC): lanes that reach the
+// budget keep going with their position pinned at lim, so their bits land in
+// the slot's spare words and no per-lane predication is needed.  PLIM = true:
+// a lane stops at its precision limit, so its state is updated under `act`.
+template <int PREC, bool PLIM>
 __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, uint32_t pos, uint32_t lim,
                                                 uint32_t maxprec, const uint32_t (&Pl)[PREC],
                                                 const uint32_t (&Ph)[PREC])
 {
   const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
-  uint32_t n = 0, Sl = 0, Sh = 0;
+  uint32_t* const dm1 = s.d() - 1;  // dword j-1 of a position with j = ceil(p / 32)
+  const uint32_t lim31 = lim + 31u;
+  uint32_t p31 = pos + 31u;  // position + 31: j = p31 >> 5, alignbit shift = 31 - p31
+  uint32_t n = 0, nn = ~0u, Sl = 0, Sh = 0;
+  ExtEvent e0{0, 0, 0, 0}, e1{0, 0, 0, 0}, e2{0, 0, 0, 0};
+#ifdef ZFP_PLANE_UNROLL
+#pragma unroll ZFP_PLANE_UNROLL
+#else
+#pragma unroll
+#endif
   for (int k = PREC - 1; k >= 0; k--) {
-    const bool act = pos < lim && (uint32_t)k >= kmin;
-    if (!__any(act))
+    const bool act = p31 < lim31 && (!PLIM || (uint32_t)k >= kmin);
+    if (__builtin_amdgcn_ballot_w64(act) == 0)
       break;
-    const int ku = __builtin_amdgcn_readfirstlane(k);
-    const uint32_t pl = Pl[ku], ph = Ph[ku];
+    const uint32_t pl = Pl[k], ph = Ph[k];
     const uint32_t Nl = pl & ~Sl, Nh = ph & ~Sh;
     const uint64_t N = ((uint64_t)Nh << 32) | Nl;
     const bool nz = N != 0;
     const uint32_t clz = (uint32_t)__clzll((long long)(N | 1ull));  // of N when nz
     const uint32_t n1 = nz ? 64u - clz : n;
     const uint64_t S1 = nz ? (~0ull >> clz) : (((uint64_t)Sh << 32) | Sl);
-    const uint32_t t2 = (uint32_t)__popc(Nh) + (uint32_t)__popc(Nl) + n1;  // n' + c
-    const uint32_t impl = Nh >> 31;                                       // top one is coefficient 63
-    const uint32_t len = t2 + 1u - (uint32_t)(S1 >> 63) - impl;
+    const uint32_t t2 = (uint32_t)__popc(Nh) + ((uint32_t)__popc(Nl) + n1);  // n' + c
+    const uint32_t impl = Nh >> 31;                                         // top one is coefficient 63
     const uint64_t xs = N >> (n & 63u);  // n == 64 only with N == 0
     const uint32_t x0 = (uint32_t)xs;
     const uint32_t b0 = x0 & 0xffu;
     const uint32_t d16 = lut[b0] | (lut[(x0 >> 8) & 0xffu] << (8u + (uint32_t)__popc(b0)));
-    const uint32_t m = (2u + impl) << ((t2 - n - 1u) & 31u);
+    const uint32_t m = (2u | impl) << ((t2 + nn) & 31u);  // surplus of the top pair at h + c
     uint32_t g = ((d16 << 1) | (nz ? 1u : 0u)) - m;
-    const uint32_t h = n1 - n - 1u;  // top one of xs (when nz)
+    const uint32_t h = n1 + nn;  // top one of xs (when nz)
     const bool ext = act && nz && h >= 16u;
-    if (__any(ext)) {
-      // the top one lies beyond the first unit: undo the surplus removal and
-      // expand units 1..3 at their dbl offsets
-      const uint32_t gp = pos + n;
-      uint32_t D = 16u + (uint32_t)__popc(x0 & 0xffffu);  // dbl length of unit 0
-      if (ext)
-        g += m;
-#pragma unroll
-      for (int j = 1; j < 4; j++) {
-        // lanes whose top one lies below this unit take no part (the branch is
-        // entered for the wave, so every per-lane effect is predicated here)
-        const bool unit = ext && h >= 16u * j;
-        if (__any(unit)) {
-          const uint32_t u = (uint32_t)(xs >> (16 * j)) & 0xffffu;
-          const uint32_t cu = (uint32_t)__popc(u);
-          uint32_t dj = dbl16(lut, u);
-          if (h < 16u * (j + 1))  // the top one is in this unit
-            dj -= (2u + impl) << ((h - 16u * j + cu - 1u) & 31u);
-          if (unit) {
-            if (j == 1)  // also carries bit 32 of g (unit 0 all ones)
-              s.put64_clamped(gp + D, (dj << 1) | (d16 >> 31), dj >> 31);
-            else
-              s.put32_clamped(gp + 1u + D, dj);
-          }
-          D += 16u + cu;
-        }
+    if (__builtin_amdgcn_ballot_w64(ext) != 0) {
+      if (ext) {
+        g += m;  // the top pair is not in unit 0
+        e2 = e1;
+        e1 = e0;
+        e0 = ExtEvent{p31 - 31u + n, x0, (uint32_t)(xs >> 32), h | (impl << 6) | ((d16 >> 31) << 7)};
       }
     }
-    if (act) {
-      s.put64(pos, pl ^ Nl, ph ^ Nh);  // the n verbatim bits
-      s.put32(pos + n, g);
-      pos += len;
+    const int32_t dlen = (int32_t)t2 + 1 + ((int32_t)(uint32_t)(S1 >> 32) >> 31) + ((int32_t)Nh >> 31);
+    if (PLIM) {
+      if (act) {
+        s.put64(p31 - 31u, pl ^ Nl, ph ^ Nh);  // the n verbatim bits
+        s.put32(p31 - 31u + n, g);
+      }
+      p31 = act ? p31 + (uint32_t)dlen : p31;
+      n = act ? n1 : n;
+      Sl = act ? (uint32_t)S1 : Sl;
+      Sh = act ? (uint32_t)(S1 >> 32) : Sh;
+    } else {
+      {
+        uint32_t* q = dm1 + (p31 >> 5);
+        const uint32_t t = 31u - p31;
+        const uint32_t v0 = pl ^ Nl, v1 = ph ^ Nh;
+        lds_or32(q, __builtin_amdgcn_alignbit(v0, 0u, t));
+        lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
+        lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
+      }
+      {
+        const uint32_t pg = p31 + n;
+        uint32_t* q = dm1 + (pg >> 5);
+        const uint32_t t = 31u - pg;
+        lds_or32(q, __builtin_amdgcn_alignbit(g, 0u, t));
+        lds_or32(q + 1, __builtin_amdgcn_alignbit(0u, g, t));
+      }
+      p31 += (uint32_t)dlen;
+      p31 = p31 < lim31 ? p31 : lim31;
       n = n1;
       Sl = (uint32_t)S1;
       Sh = (uint32_t)(S1 >> 32);
     }
+    nn = ~n;
   }
-  return pos < lim ? pos : lim;
+  if (__any(e0.hb >= 16u)) {
+    expand_event(s, lut, e0);
+    if (__any(e1.hb >= 16u)) {
+      expand_event(s, lut, e1);
+      if (__any(e2.hb >= 16u))
+        expand_event(s, lut, e2);
+    }
+  }
+  const uint32_t end = p31 - 31u;
+  return end < lim ? end : lim;
 }
 
 // Decoder twin (decode.c:69-246), including the reference quirk that a

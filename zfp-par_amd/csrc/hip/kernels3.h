@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256, 4) void encode3_aligned(const S* __restrict__ 
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
     OrSlot os{wslot + (size_t)lane * swp, 2 * swp - 1};
-    encode_block3<S, REV>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
+    encode_block3<S, REV, true>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
   if (first >= g.nblocks)
     return;
@@ -199,6 +199,10 @@ __device__ __forceinline__ uint64_t lookback(uint64_t* status, uint64_t w, uint3
   return excl;
 }
 
+template <int NB>
+__device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
+                                          const uint32_t* wrt, uint64_t w, uint64_t start, uint32_t total);
+
 template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        GeneralArgs a)
@@ -264,8 +268,19 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   __syncthreads();
   if (!live)
     return;
+  pack_wave<64>(a, wbase, off, wrt, w, start, total);
+}
 
-  // gather stream words of [G, G + total), G = g0 + start
+// Pack the NB block slots of one wave (bit lengths wrt[], bit offsets off[]
+// relative to the wave's first bit) into the stream words of [G, G + total),
+// G = g0 + start: interior words are plain stores, the first and last word
+// (shared with the neighbouring waves) go to the partials for the fix-up
+// kernels.  Shared by encode3_general (NB = 64) and encode4 (NB = 16).
+template <int NB>
+__device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
+                                          const uint32_t* wrt, uint64_t w, uint64_t start, uint32_t total)
+{
+  const int lane = threadIdx.x & 63;
   const uint64_t G = a.g0 + start;
   const uint64_t W0 = G >> 6;
   const uint32_t r0 = (uint32_t)(G & 63);
@@ -276,10 +291,10 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
     // local bit range of this word relative to the wave's first bit
     int64_t lo = (int64_t)o * 64 - r0;
     int64_t hi = lo + 64;
-    // first lane whose block ends after lo
+    // first block that ends after lo
     int l = 0;
     {
-      int lo_i = 0, hi_i = 63;
+      int lo_i = 0, hi_i = NB - 1;
       int64_t key = lo < 0 ? 0 : lo;
       while (lo_i < hi_i) {
         int mid = (lo_i + hi_i + 1) >> 1;
@@ -289,7 +304,7 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
       l = lo_i;
     }
     uint64_t val = 0;
-    for (; l < 64 && (int64_t)off[l] < hi; l++) {
+    for (; l < NB && (int64_t)off[l] < hi; l++) {
       int64_t s0 = off[l];
       int64_t s1 = s0 + wrt[l];
       int64_t x0 = s0 > lo ? s0 : lo;

@@ -1,0 +1,175 @@
+// 4D encode/decode kernels: one 4x4x4x4 block per quad of lanes (block4.h),
+// 16 blocks per wave, one wave per 64-thread workgroup.  The per-block LDS
+// exchange area of the w-lift is what limits occupancy, so workgroups are kept
+// to one wave and the CU packs as many as its LDS holds.
+//
+//  encode4  every mode; blocks are packed at their bit offsets exactly as by
+//           encode3_general (fixed rate: analytic offsets; variable rate:
+//           decoupled look-back over per-wave bit totals + block index), the
+//           words shared with neighbouring waves go to the fix-up kernels.
+//  decode4  stages the wave's 16 blocks in LDS (fixed rate: analytic offsets;
+//           variable rate: from the index), each quad decodes its block.
+#pragma once
+
+#include "block4.h"
+#include "kernels3.h"
+
+namespace zfp_amd {
+
+constexpr uint32_t kBlocks4PerWave = 16;
+// LDS words ahead of the slot / exchange region.  Encoder: doubled-ones table
+// (256 dwords), order table (64), per-block offsets and written counts (16+16).
+constexpr uint32_t kEnc4HeadWords = (256 + 64 + 16 + 16) / 2;
+// Decoder: order table (64 dwords), per-block stream bit offsets (16).
+constexpr uint32_t kDec4HeadWords = (64 + 16) / 2;
+
+// Slot of a 4D block with budget `lim` bits: its dwords plus two spare dwords
+// (targets of the clamped writes past the budget); odd, so the 16 slots of a
+// wave start on different banks.
+__host__ __device__ constexpr uint32_t slot_words4(uint32_t lim) { return ((((lim + 31u) >> 5) + 3u) / 2u) | 1u; }
+
+template <typename S, bool VEC, bool REV>
+__global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geometry g, CodecParams cp, GeneralArgs a)
+{
+  using Int = typename Traits<S>::Int;
+  extern __shared__ uint64_t lds[];
+  uint32_t* lut = reinterpret_cast<uint32_t*>(lds);
+  uint32_t* tab = lut + 256;
+  uint32_t* off = tab + 64;
+  uint32_t* wrt = off + kBlocks4PerWave;
+  uint64_t* region = lds + kEnc4HeadWords;
+  const uint32_t lane = threadIdx.x;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++)
+    lut[lane + 64 * i] = dbl_entry(lane + 64 * i);
+  tab[lane] = kOrderTab4.t[lane];
+
+  const uint64_t nwaves = (g.nblocks + kBlocks4PerWave - 1) / kBlocks4PerWave;
+  uint64_t w;
+  if (a.var) {
+    uint32_t t = 0;
+    if (lane == 0)
+      t = atomicAdd(a.ticket, 1u);
+    w = (uint64_t)__shfl(t, 0, 64);
+  } else {
+    w = blockIdx.x;
+  }
+  const bool live = w < nwaves;
+  const uint64_t first = w * kBlocks4PerWave;
+  const uint32_t qd = lane >> 2, r = lane & 3u;
+  const uint64_t b = first + qd;
+  const bool valid = live && b < g.nblocks;
+  BlockPos ps{};
+  S v[64];
+  if (valid) {
+    const BlockPos p = block_pos(g, b, 4);
+    ps = slice_pos(g, p, pad_src_w((int)r, p.cnt[3]));
+    gather3<S, VEC>(v, data, g, ps);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      v[i] = 0;
+  }
+  __syncthreads();
+  uint32_t* d = reinterpret_cast<uint32_t*>(region + (size_t)qd * a.swp);
+  Int* X = reinterpret_cast<Int*>(region) + (size_t)qd * kXStride;
+  uint32_t len = encode_block4<S, REV>(d, 2 * a.swp - 1, lut, tab, X, region, kBlocks4PerWave * a.swp, v, cp,
+                                       [&](S (&rr)[64]) {
+                                         if (valid) {
+                                           gather3<S, VEC>(rr, data, g, ps);
+                                         } else {
+#pragma unroll
+                                           for (int i = 0; i < 64; i++)
+                                             rr[i] = 0;
+                                         }
+                                       });
+  len = valid ? len : 0u;
+  const uint32_t lq = r == 0u ? len : 0u;  // the quad's lanes agree on len
+  const uint32_t incl = wave_incl_scan(lq);
+  const uint32_t total = __shfl(incl, 63, 64);
+  if (r == 0u) {
+    off[qd] = incl - lq;
+    wrt[qd] = len < 64 * a.swp ? len : 64 * a.swp;
+  }
+  uint64_t start = 0;
+  if (!live) {
+  } else if (a.var) {
+    uint64_t e = 0;
+    if (lane == 0)
+      e = lookback(a.status, w, total, a.error);
+    start = __shfl(e, 0, 64);
+    if (a.idx_len && valid && r == 0u)
+      a.idx_len[b] = (uint16_t)len;
+    if (lane == 0) {
+      if (a.idx_base)
+        a.idx_base[w] = start;
+      if (w == nwaves - 1)
+        *a.total_bits = start + total;
+    }
+  } else {
+    start = first * (uint64_t)a.maxbits;
+  }
+  __syncthreads();
+  if (!live)
+    return;
+  pack_wave<kBlocks4PerWave>(a, region, off, wrt, w, start, total);
+}
+
+template <typename S, bool VEC, bool REV>
+__global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
+{
+  using Int = typename Traits<S>::Int;
+  extern __shared__ uint64_t lds[];
+  uint32_t* tab = reinterpret_cast<uint32_t*>(lds);
+  uint32_t* sbit = tab + 64;
+  uint64_t* region = lds + kDec4HeadWords;
+  const uint32_t lane = threadIdx.x;
+  tab[lane] = kOrderTab4.t[lane];
+  const uint64_t w = blockIdx.x;
+  const uint64_t first = w * kBlocks4PerWave;
+  const uint32_t qd = lane >> 2, r = lane & 3u;
+  const uint64_t b = first + qd;
+  const bool valid = b < g.nblocks;
+  uint64_t start;
+  uint32_t pos;
+  if (a.var) {
+    const uint32_t len = (valid && r == 0u) ? a.idx_len[b] : 0u;
+    pos = wave_incl_scan(len) - len;
+    start = a.idx_base[w];
+  } else {
+    pos = qd * a.maxbits;
+    start = first * (uint64_t)a.maxbits;
+  }
+  const uint64_t G = a.g0 + start;
+  const uint64_t W0 = G >> 6;
+  if (r == 0u)
+    sbit[qd] = (uint32_t)(G & 63) + pos;
+  __syncthreads();
+  const uint64_t left = g.nblocks - first;
+  const uint32_t nb = left < kBlocks4PerWave ? (uint32_t)left : kBlocks4PerWave;
+  const uint32_t pairs = nb * a.W;
+  for (uint32_t t = lane; t < pairs; t += 64) {
+    const uint32_t l = __umulhi(t, a.wmagic);
+    const uint32_t j = t - l * a.W;
+    const uint32_t sb = sbit[l];
+    const uint64_t gw = W0 + (sb >> 6) + j;
+    const uint32_t sh = sb & 63;
+    const uint64_t lo = gw < a.in_words ? a.in[gw] : 0ull;
+    const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
+    region[(size_t)l * a.swp + j] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+  }
+  __syncthreads();
+  WordReader rd;
+  rd.w = region + (size_t)qd * a.swp;
+  rd.pos = 0;
+  S v[64];
+  Int* X = reinterpret_cast<Int*>(region) + (size_t)qd * kXStride;
+  decode_block4<S, REV>(rd, v, cp, X, tab, valid);
+  if (!valid)
+    return;
+  const BlockPos p = block_pos(g, b, 4);
+  if ((int)r < p.cnt[3])
+    scatter3<S, VEC>(v, data, g, slice_pos(g, p, (int)r));
+}
+
+}  // namespace zfp_amd

@@ -9,6 +9,8 @@
 //   everything else (variable rate, odd block sizes) -> encode3_general with
 //        decoupled look-back, then fixup_zero/fixup_or for words shared by waves
 //   decode: decode3 (fixed-rate offsets analytic, variable rate from the index)
+//   4D: encode4 / decode4 (one block per quad of lanes, 16 blocks per wave),
+//        every mode through the packing path of encode3_general
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -19,7 +21,7 @@
 #include <string>
 #include <vector>
 
-#include "kernels3.h"
+#include "kernels4.h"
 #include "zfp_hip.h"
 
 using namespace zfp_amd;
@@ -154,8 +156,8 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
     return fail("null job");
   if (j->type != 3 && j->type != 4)
     return fail("zfp_hip: scalar type %d not supported (float and double only)", j->type);
-  if (j->dims != 3)
-    return fail("zfp_hip: %dD fields not supported yet (3D only)", j->dims);
+  if (j->dims != 3 && j->dims != 4)
+    return fail("zfp_hip: %dD fields are not on the MI355X path (3D and 4D only)", j->dims);
   p.dims = j->dims;
   p.dbl = j->type == 4;
   p.cp.minbits = j->minbits;
@@ -181,7 +183,10 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
     p.g.nblocks *= nb;
     if (a < p.dims && e > p.g.f[a]) {
       int64_t d0 = (int64_t)p.g.f[a] * p.g.s[a];
-      int64_t d1 = (int64_t)(e - 1) * p.g.s[a];
+      // a block reads whole 4-blocks past a chunk end that is not block aligned
+      // (up to the field edge, compress.c:127-133): the span covers them
+      const uint64_t eb = std::min<uint64_t>(p.g.n[a], p.g.f[a] + 4 * nb);
+      int64_t d1 = (int64_t)(eb - 1) * p.g.s[a];
       p.span_lo += std::min(d0, d1);
       p.span_hi += std::max(d0, d1);
     }
@@ -189,7 +194,8 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
   const int ebits = p.dbl ? 11 : 8, pbits = p.dbl ? 6 : 5, intprec = p.dbl ? 64 : 32;
   const bool rev = p.cp.minexp < kMinExp;
   const uint32_t hdr = rev ? 2 + ebits + pbits : 1 + ebits;
-  uint64_t body = hdr + 63 + 64ull * std::min<uint32_t>(p.cp.maxprec, intprec);
+  const uint64_t bvals = p.dims == 4 ? 256 : 64;  // values per block
+  uint64_t body = hdr + (bvals - 1) + bvals * std::min<uint32_t>(p.cp.maxprec, intprec);
   uint64_t bound = body;
   if (p.cp.maxbits >= hdr)
     bound = std::min<uint64_t>(bound, p.cp.maxbits);
@@ -198,7 +204,9 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
   p.fixed = !rev && p.cp.minbits == p.cp.maxbits && p.cp.maxbits >= (uint32_t)(1 + ebits);
   const size_t es = p.dbl ? 8 : 4;
   p.vec = p.g.s[0] == 1 && (p.g.s[1] % 4) == 0 && (p.g.s[2] % 4) == 0 && (p.g.f[0] % 4) == 0 &&
-          ((uintptr_t)field_base % (4 * es)) == 0;
+          (p.dims < 4 || (p.g.s[3] % 4) == 0) && ((uintptr_t)field_base % (4 * es)) == 0;
+  if (!p.fixed && p.max_len > 0xffff)
+    return fail("zfp_hip: block length bound %u bits exceeds the block index (16-bit lengths)", p.max_len);
   return 1;
 }
 
@@ -209,16 +217,127 @@ static size_t slot_words_odd(uint32_t bits)
 
 // ---------------------------------------------------------------------------
 // launchers
+
+// Arguments of the packing encoders (encode3_general, encode4) for `nwaves`
+// waves: fix-up partials, look-back state and, for a variable-rate stream with
+// an index, the index buffers.  Queues the look-back resets on the stream.
+static int general_args(Ctx* c, const Plan& p, uint64_t nwaves, uint32_t swp, uint64_t* d_out, uint32_t g0,
+                        zfp_hip_index* index, GeneralArgs& a)
+{
+  const bool var = !p.fixed;
+  // misc: [0] total bits, [1] ticket|error
+  if (!ensure(c->partials, nwaves * 2 * sizeof(Partial)) || !ensure(c->misc, 64) ||
+      (var && !ensure(c->status, nwaves * 8)))
+    return 0;
+  a = GeneralArgs{};
+  a.out = d_out;
+  a.g0 = g0;
+  a.swp = swp;
+  a.var = var ? 1 : 0;
+  a.maxbits = p.cp.maxbits;
+  a.status = (uint64_t*)c->status.p;
+  a.total_bits = (uint64_t*)c->misc.p;
+  a.ticket = (uint32_t*)((char*)c->misc.p + 8);
+  a.error = (uint32_t*)((char*)c->misc.p + 12);
+  a.partials = (Partial*)c->partials.p;
+  if (var && index) {
+    if (index->cap_blocks < p.g.nblocks) {
+      if (index->d_len) (void)hipFree(index->d_len);
+      index->d_len = nullptr;
+      HIP_TRY(hipMalloc(&index->d_len, p.g.nblocks * sizeof(uint16_t)));
+      index->cap_blocks = p.g.nblocks;
+    }
+    if (index->cap_waves < nwaves) {
+      if (index->d_base) (void)hipFree(index->d_base);
+      index->d_base = nullptr;
+      HIP_TRY(hipMalloc(&index->d_base, nwaves * sizeof(uint64_t)));
+      index->cap_waves = nwaves;
+    }
+    index->device = c->device;
+    index->nblocks = p.g.nblocks;
+    index->nwaves = nwaves;
+    a.idx_len = index->d_len;
+    a.idx_base = index->d_base;
+  }
+  HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, c->stream));
+  if (var)
+    HIP_TRY(hipMemsetAsync(c->status.p, 0, nwaves * 8, c->stream));
+  return 1;
+}
+
+// After a packing encoder: merge the words shared by neighbouring waves; for a
+// variable-rate stream read back its length (and the look-back health flag).
+static int finish_general(Ctx* c, const Plan& p, uint64_t nwaves, uint64_t* d_out, uint32_t g0, uint64_t head_word,
+                          const GeneralArgs& a, zfp_hip_index* index, uint64_t* total_bits)
+{
+  unsigned fg = (unsigned)((2 * nwaves + 255) / 256);
+  hipLaunchKernelGGL(fixup_zero, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out, 0ull,
+                     g0 ? head_word : 0ull);
+  hipLaunchKernelGGL(fixup_or, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out);
+  HIP_TRY(hipGetLastError());
+  if (!p.fixed) {
+    uint64_t host[2] = {0, 0};
+    HIP_TRY(hipMemcpyAsync(host, c->misc.p, 16, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((uint32_t)(host[1] >> 32))
+      return fail("zfp_hip: look-back timed out (GPU scheduling anomaly)");
+    *total_bits = host[0];
+    if (index)
+      index->total_bits = host[0];
+  } else {
+    *total_bits = p.g.nblocks * (uint64_t)p.cp.maxbits;
+  }
+  return 1;
+}
+
+// 4D: encode4 for every mode (one 64-thread workgroup per 16 blocks)
+template <typename S>
+static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out, uint32_t g0,
+                          uint64_t head_word, zfp_hip_index* index, uint64_t* total_bits)
+{
+  using Int = typename Traits<S>::Int;
+  const uint64_t nwaves = (p.g.nblocks + kBlocks4PerWave - 1) / kBlocks4PerWave;
+  if (nwaves > 0x7fffffffull)
+    return fail("zfp_hip: field too large for one launch");
+  const uint32_t swp = slot_words4(p.bound_bits);
+  const size_t region = std::max<size_t>((size_t)kBlocks4PerWave * swp * 8,
+                                         (size_t)kBlocks4PerWave * kXStride * sizeof(Int));
+  const size_t lds = (size_t)kEnc4HeadWords * 8 + region;
+  if (lds > 160 * 1024)
+    return fail("zfp_hip: 4D block bound %u bits too large for LDS", p.bound_bits);
+  GeneralArgs a{};
+  if (!general_args(c, p, nwaves, swp, d_out, g0, index, a))
+    return 0;
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  dim3 grid((unsigned)nwaves), block(64);
+  const bool rev = p.cp.minexp < kMinExp;
+  if (p.vec && rev)
+    hipLaunchKernelGGL((encode4<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (p.vec)
+    hipLaunchKernelGGL((encode4<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (rev)
+    hipLaunchKernelGGL((encode4<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else
+    hipLaunchKernelGGL((encode4<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  return finish_general(c, p, nwaves, d_out, g0, head_word, a, index, total_bits);
+}
+
 template <typename S>
 static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out, uint32_t g0,
                          uint64_t head_word, zfp_hip_index* index, uint64_t* total_bits)
 {
+  if (p.dims == 4)
+    return launch_encode4<S>(c, p, d_field, d_out, g0, head_word, index, total_bits);
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
   if (ngroups > 0x7fffffffull)
     return fail("zfp_hip: field too large for one launch");
   dim3 grid((unsigned)ngroups), block(256);
-  if (p.fixed && (p.cp.maxbits % 64) == 0) {
+  // aligned fixed-rate kernel: word-multiple blocks and no precision limit
+  // below the integer width (its coder runs every plane until the budget)
+  if (p.fixed && (p.cp.maxbits % 64) == 0 && p.cp.maxprec >= (p.dbl ? 64u : 32u)) {
     const uint32_t sw = p.cp.maxbits / 64;
     const uint32_t swp = (uint32_t)slot_words_odd(p.cp.maxbits);  // words from sw on are spare
     const uint32_t magic = sw > 1 ? (uint32_t)((0x100000000ull + sw - 1) / sw) : 0u;
@@ -254,44 +373,9 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   size_t lds = (size_t)kWavesPerGroup * (64 * swp + 64) * 8;
   if (lds + kLutBytes > 160 * 1024)
     return fail("zfp_hip: block bound %u bits too large for LDS", p.bound_bits);
-  const bool var = !p.fixed;
-  // misc: [0] total bits, [1] ticket|error
-  if (!ensure(c->partials, nwaves * 2 * sizeof(Partial)) || !ensure(c->misc, 64) ||
-      (var && !ensure(c->status, nwaves * 8)))
-    return 0;
   GeneralArgs a{};
-  a.out = d_out;
-  a.g0 = g0;
-  a.swp = swp;
-  a.var = var ? 1 : 0;
-  a.maxbits = p.cp.maxbits;
-  a.status = (uint64_t*)c->status.p;
-  a.total_bits = (uint64_t*)c->misc.p;
-  a.ticket = (uint32_t*)((char*)c->misc.p + 8);
-  a.error = (uint32_t*)((char*)c->misc.p + 12);
-  a.partials = (Partial*)c->partials.p;
-  if (var && index) {
-    if (index->cap_blocks < p.g.nblocks) {
-      if (index->d_len) (void)hipFree(index->d_len);
-      index->d_len = nullptr;
-      HIP_TRY(hipMalloc(&index->d_len, p.g.nblocks * sizeof(uint16_t)));
-      index->cap_blocks = p.g.nblocks;
-    }
-    if (index->cap_waves < nwaves) {
-      if (index->d_base) (void)hipFree(index->d_base);
-      index->d_base = nullptr;
-      HIP_TRY(hipMalloc(&index->d_base, nwaves * sizeof(uint64_t)));
-      index->cap_waves = nwaves;
-    }
-    index->device = c->device;
-    index->nblocks = p.g.nblocks;
-    index->nwaves = nwaves;
-    a.idx_len = index->d_len;
-    a.idx_base = index->d_base;
-  }
-  HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, c->stream));
-  if (var)
-    HIP_TRY(hipMemsetAsync(c->status.p, 0, nwaves * 8, c->stream));
+  if (!general_args(c, p, nwaves, swp, d_out, g0, index, a))
+    return 0;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   const bool rev = p.cp.minexp < kMinExp;
   if (p.vec && rev)
@@ -304,23 +388,52 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
     hipLaunchKernelGGL((encode3_general<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  unsigned fg = (unsigned)((2 * nwaves + 255) / 256);
-  hipLaunchKernelGGL(fixup_zero, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out, 0ull,
-                     g0 ? head_word : 0ull);
-  hipLaunchKernelGGL(fixup_or, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out);
-  HIP_TRY(hipGetLastError());
-  if (var) {
-    uint64_t host[2] = {0, 0};
-    HIP_TRY(hipMemcpyAsync(host, c->misc.p, 16, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if ((uint32_t)(host[1] >> 32))
-      return fail("zfp_hip: look-back timed out (GPU scheduling anomaly)");
-    *total_bits = host[0];
-    if (index)
-      index->total_bits = host[0];
-  } else {
-    *total_bits = p.g.nblocks * (uint64_t)p.cp.maxbits;
+  return finish_general(c, p, nwaves, d_out, g0, head_word, a, index, total_bits);
+}
+
+template <typename S>
+static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
+                          const zfp_hip_index* index)
+{
+  using Int = typename Traits<S>::Int;
+  const uint64_t nwaves = (p.g.nblocks + kBlocks4PerWave - 1) / kBlocks4PerWave;
+  if (nwaves > 0x7fffffffull)
+    return fail("zfp_hip: field too large for one launch");
+  DecodeArgs a{};
+  a.in = d_in;
+  a.in_words = in_words;
+  a.g0 = g0;
+  a.var = p.fixed ? 0 : 1;
+  a.maxbits = p.cp.maxbits;
+  const uint32_t per_block = p.fixed ? p.cp.maxbits : p.max_len;
+  a.W = (per_block + 63) / 64 + 1;  // peek64 at the budget end reads one word past it
+  a.swp = a.W | 1;
+  a.wmagic = (uint32_t)((0x100000000ull + a.W - 1) / a.W);
+  if (!p.fixed) {
+    if (index->nwaves != nwaves)
+      return fail("zfp_hip: block index has %llu waves, the 4D layout needs %llu", (unsigned long long)index->nwaves,
+                  (unsigned long long)nwaves);
+    a.idx_len = index->d_len;
+    a.idx_base = index->d_base;
   }
+  const size_t region = std::max<size_t>((size_t)kBlocks4PerWave * a.swp * 8,
+                                         (size_t)kBlocks4PerWave * kXStride * sizeof(Int));
+  const size_t lds = (size_t)kDec4HeadWords * 8 + region;
+  if (lds > 160 * 1024)
+    return fail("zfp_hip: 4D block size too large for LDS staging (%u bits)", per_block);
+  dim3 grid((unsigned)nwaves), block(64);
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  const bool rev = p.cp.minexp < kMinExp;
+  if (p.vec && rev)
+    hipLaunchKernelGGL((decode4<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (p.vec)
+    hipLaunchKernelGGL((decode4<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (rev)
+    hipLaunchKernelGGL((decode4<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else
+    hipLaunchKernelGGL((decode4<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   return 1;
 }
 
@@ -328,7 +441,12 @@ template <typename S>
 static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
                          const zfp_hip_index* index)
 {
+  if (p.dims == 4)
+    return launch_decode4<S>(c, p, d_field, d_in, in_words, g0, index);
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
+  if (!p.fixed && index->nwaves != nwaves)
+    return fail("zfp_hip: block index has %llu waves, the 3D layout needs %llu", (unsigned long long)index->nwaves,
+                (unsigned long long)nwaves);
   const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
   DecodeArgs a{};
   a.in = d_in;

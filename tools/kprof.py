@@ -26,6 +26,19 @@ def field(torch, n, dtype, dev):
     return out
 
 
+def field4(torch, n, dtype, dev):
+    """F1 with the C5 w term: + .25 cos(.04 w)."""
+    import math
+    x = torch.arange(n, device=dev, dtype=torch.float64)
+    base = torch.sin(0.05 * x)[None, :] * torch.cos(0.03 * x)[:, None]
+    xy = 0.01 * x[None, :] * x[:, None] / n
+    z = x[:, None, None]
+    out = torch.empty((n, n, n, n), device=dev, dtype=dtype)
+    for w in range(n):
+        out[w] = (base[None] + 0.5 * torch.sin(0.02 * z + xy[None]) + 0.25 * math.cos(0.04 * w)).to(dtype)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="rate")
@@ -34,6 +47,7 @@ def main():
     ap.add_argument("--n", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--decode", action="store_true")
+    ap.add_argument("--dims", type=int, default=3)
     a = ap.parse_args()
     import torch
     from capi import ZfpCAPI
@@ -43,10 +57,14 @@ def main():
     dev = torch.device("cuda", 0)
     dt = torch.float32 if a.dtype == "f32" else torch.float64
     zt = 3 if a.dtype == "f32" else 4
-    f = field(torch, a.n, dt, dev)
-    zf = lib.zfp_field_3d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.n)
+    if a.dims == 4:
+        f = field4(torch, a.n, dt, dev)
+        zf = lib.zfp_field_4d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.n, a.n)
+    else:
+        f = field(torch, a.n, dt, dev)
+        zf = lib.zfp_field_3d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.n)
     zs = lib.zfp_stream_open(None)
-    api.set_mode(zs, a.mode, a.param if a.mode != "reversible" else None, zt, 3)
+    api.set_mode(zs, a.mode, a.param if a.mode != "reversible" else None, zt, a.dims)
     cap = lib.zfp_stream_maximum_size(zs, zf)
     out = torch.zeros(cap, dtype=torch.uint8, device=dev)
     bs = lib.stream_open(ctypes.c_void_p(out.data_ptr()), cap)
@@ -60,7 +78,7 @@ def main():
         lib.zfp_hip_last_timing(ctypes.byref(k), ctypes.byref(t))
         ks.append(k.value)
     gb = f.numel() * f.element_size() / 1e9
-    print("encode %s %s %s: bytes=%d kernel_ms=%s  GB/s=%.1f" % (a.dtype, a.mode, a.param, nb,
+    print("encode %dD %s %s %s: bytes=%d kernel_ms=%s  GB/s=%.1f" % (a.dims, a.dtype, a.mode, a.param, nb,
           " ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
     if a.decode:
         back = torch.empty_like(f)

@@ -64,7 +64,7 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m
 // fix-up kernels.  Slots are swp >= slot_words_for(64 sw) words; words from sw
 // on are spare (bits past the budget) and never copied.
 template <typename S, bool VEC, bool REV>
-__global__ __launch_bounds__(256, 4) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
+__global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        uint64_t* __restrict__ out, uint32_t sw, uint32_t swp,
                                                        uint32_t magic, uint32_t r0, Partial* __restrict__ partials)
 {

@@ -112,6 +112,7 @@ int main()
   for (int a = 0; a < 4; a++) { g.n[a] = a < 3 ? n : 1; g.f[a] = 0; g.nb[a] = a < 3 ? n / 4 : 1; }
   g.s[0] = 1; g.s[1] = n; g.s[2] = n * n; g.s[3] = 0;
   g.nblocks = (n / 4) * (n / 4) * (n / 4);
+  for (int a = 0; a < 3; a++) g.dv[a] = make_fastdiv(g.nb[a]);
   CodecParams cp{1024, 1024, 64, -1074};
   const uint32_t sw = 16, swp = 19, magic = (uint32_t)((0x100000000ull + sw - 1) / sw);
   const size_t lds = 4 * 64 * swp * 8;

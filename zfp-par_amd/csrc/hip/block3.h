@@ -22,12 +22,36 @@ __device__ __forceinline__ void pad_line(S* v, int b, int s, int n)
   if (n <= 3) v[b + 3 * s] = v[b];
 }
 
+// x / d for 32-bit x by an invariant d >= 1 (round-up method: 33-bit magic
+// split into m and two shifts; exact for every x)
+struct FastDiv {
+  uint32_t m, s1, s2;
+};
+
+__host__ __device__ inline FastDiv make_fastdiv(uint32_t d)
+{
+  if (d == 0)
+    d = 1;
+  uint32_t l = 0;
+  while (l < 32 && (1ull << l) < d)
+    l++;  // ceil(log2 d)
+  const uint64_t m = ((1ull << 32) * ((1ull << l) - d)) / d + 1;
+  return FastDiv{(uint32_t)m, l < 1 ? l : 1u, l > 1 ? l - 1 : 0u};
+}
+
+__device__ __forceinline__ uint32_t fastdiv(uint32_t x, const FastDiv& f)
+{
+  const uint32_t t = __umulhi(x, f.m);
+  return (t + ((x - t) >> f.s1)) >> f.s2;
+}
+
 struct Geometry {
   uint64_t n[4];
   int64_t s[4];
   uint64_t f[4];
   uint32_t nb[4];  // blocks per axis in the chunk box
-  uint64_t nblocks;
+  FastDiv dv[3];   // division by nb[0..2] (block index -> coordinates)
+  uint64_t nblocks;  // < 2^32 (checked by the host)
 };
 
 struct BlockPos {
@@ -36,19 +60,23 @@ struct BlockPos {
   bool full;
 };
 
-__device__ __forceinline__ BlockPos block_pos(const Geometry& g, uint64_t b, int dims)
+__device__ __forceinline__ BlockPos block_pos(const Geometry& g, uint64_t b64, int dims)
 {
   BlockPos p;
   p.off = 0;
   p.full = true;
+  uint32_t b = (uint32_t)b64;
 #pragma unroll
   for (int a = 0; a < 4; a++) {
     p.cnt[a] = 4;
     if (a < dims) {
-      uint64_t nb = g.nb[a];
-      uint64_t bi = (a == dims - 1) ? b : b % nb;
-      b = (a == dims - 1) ? 0 : b / nb;
-      uint64_t x = g.f[a] + 4 * bi;
+      uint32_t bi = b;
+      if (a < dims - 1) {
+        const uint32_t q = fastdiv(b, g.dv[a]);
+        bi = b - q * g.nb[a];
+        b = q;
+      }
+      uint64_t x = g.f[a] + 4ull * bi;
       uint64_t left = g.n[a] - x;
       p.cnt[a] = left < 4 ? (int)left : 4;
       p.full = p.full && left >= 4;

@@ -191,6 +191,10 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
       p.span_hi += std::max(d0, d1);
     }
   }
+  if (p.g.nblocks >> 32)
+    return fail("zfp_hip: %llu blocks in one call (at most 2^32 - 1)", (unsigned long long)p.g.nblocks);
+  for (int a = 0; a < 3; a++)
+    p.g.dv[a] = make_fastdiv(p.g.nb[a]);
   const int ebits = p.dbl ? 11 : 8, pbits = p.dbl ? 6 : 5, intprec = p.dbl ? 64 : 32;
   const bool rev = p.cp.minexp < kMinExp;
   const uint32_t hdr = rev ? 2 + ebits + pbits : 1 + ebits;

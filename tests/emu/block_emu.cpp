@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <random>
 #include <vector>
 #include "block3.h"
@@ -60,6 +61,32 @@ static int run(const CodecParams& cp, int type, std::mt19937_64& rng, int trials
       }
       if (!same)
         len = 0xffffffffu;  // reported as an encode mismatch below
+    }
+    if (sizeof(S) == 8 && cp.maxprec <= 32 && cp.minexp >= kMinExp) {
+      // double with maxprec <= 32: the high-planes-only coder/decoder (HI)
+      S v2[64];
+      for (int i = 0; i < 64; i++) v2[i] = orig[i];
+      std::vector<uint64_t> slot2(600, 0);
+      OrSlot os2{slot2.data(), 1199};
+      uint32_t len2 = encode_block3<S, false, false, true>(os2, lut, v2, cp, [&](S (&r)[64]) { for (int i = 0; i < 64; i++) r[i] = orig[i]; });
+      bool same = len2 == len;
+      for (uint32_t i = 0; same && i < (len + 63) / 64; i++) {
+        uint64_t m = (i == len / 64 && (len & 63)) ? ((1ull << (len & 63)) - 1) : ~0ull;
+        same = (slot2[i] & m) == (slot[i] & m);
+      }
+      S dh[64];
+      const bool any_all = emu_any_all;
+      emu_any_all = false;
+      WordReader rh{slot2.data(), 0};
+      uint32_t usedh = decode_block3<S, false, true>(rh, sq, dh, cp);
+      emu_any_all = any_all;
+      S dref[64];
+      WordReader rr{slot.data(), 0};
+      emu_any_all = false;
+      decode_block3<S, false>(rr, sq, dref, cp);
+      emu_any_all = any_all;
+      if (!same || usedh != len || std::memcmp(dh, dref, sizeof dh) != 0)
+        len = 0xfffffffeu;  // reported as an encode mismatch below
     }
     bool ok = len == oend;
     for (uint32_t i = 0; ok && i < (len + 63) / 64; i++) {

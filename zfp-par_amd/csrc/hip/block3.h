@@ -297,6 +297,42 @@ __device__ __forceinline__ void coeffs_from_planes(int64_t (&q)[64], const uint6
   }
 }
 
+// double, planes 32..63 only (the HI coder): Pl[k] = plane 32 + k
+template <bool P3 = true>
+__device__ __forceinline__ void planes_hi(uint32_t (&Pl)[32], uint32_t (&Ph)[32], const int64_t (&q)[64])
+{
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    uint64_t u0 = ((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    uint64_t u1 = ((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    Pl[i] = (uint32_t)(u0 >> 32);
+    Ph[i] = (uint32_t)(u1 >> 32);
+  }
+  transpose32(Pl);
+  transpose32(Ph);
+}
+
+// twin of planes_hi: coefficients from planes 32..63 (low planes zero)
+template <bool P3 = true>
+__device__ __forceinline__ void coeffs_from_planes_hi(int64_t (&q)[64], const uint64_t (&P)[32])
+{
+  uint32_t a[32], b[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) {
+    a[k] = (uint32_t)P[k];
+    b[k] = (uint32_t)(P[k] >> 32);
+  }
+  transpose32(a);
+  transpose32(b);
+#pragma unroll
+  for (int i = 0; i < 32; i++) {
+    uint64_t u0 = (uint64_t)a[i] << 32;
+    uint64_t u1 = (uint64_t)b[i] << 32;
+    q[P3 ? kPerm3[i] : i] = (int64_t)((u0 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+    q[P3 ? kPerm3[i + 32] : i + 32] = (int64_t)((u1 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+  }
+}
+
 __device__ __forceinline__ uint32_t precision3(int emax, const CodecParams& cp)
 {
   int p = emax - cp.minexp + 2 * 3 + 2;
@@ -306,33 +342,49 @@ __device__ __forceinline__ uint32_t precision3(int emax, const CodecParams& cp)
 
 // integer part of the block: order, planes, coder (encode.c:260-280).
 // Codes from bit `pos` of the slot; returns the end position (<= lim).
-template <bool PLIM, typename Int>
+// HI (double with maxprec <= 32): only planes 32..63 can be coded (kmin >= 32),
+// so the 32-plane coder runs on the high words -- its kmin = 32 - prec is the
+// same cut -- and the low planes are never built: half the plane registers.
+template <bool PLIM, bool HI = false, typename Int>
 __device__ __forceinline__ uint32_t encode_ints3(OrSlot& w, const uint32_t* lut, Int (&q)[64], uint32_t pos,
                                                  uint32_t lim, uint32_t prec)
 {
   using S = typename std::conditional<sizeof(Int) == 4, float, double>::type;
   constexpr int PREC = Traits<S>::kIntPrec;
-  uint32_t Pl[PREC], Ph[PREC];
-  if constexpr (PREC == 32)
-    planes_from_coeffs(Pl, Ph, q);
-  else
-    planes_from_coeffs(Pl, Ph, q, prec > 32);
-  return code_planes<PREC, PLIM>(w, lut, pos, lim, prec, Pl, Ph);
+  if constexpr (HI && PREC == 64) {
+    uint32_t Pl[32], Ph[32];
+    planes_hi(Pl, Ph, q);
+    return code_planes<32, PLIM>(w, lut, pos, lim, prec, Pl, Ph);
+  } else {
+    uint32_t Pl[PREC], Ph[PREC];
+    if constexpr (PREC == 32)
+      planes_from_coeffs(Pl, Ph, q);
+    else
+      planes_from_coeffs(Pl, Ph, q, prec > 32);
+    return code_planes<PREC, PLIM>(w, lut, pos, lim, prec, Pl, Ph);
+  }
 }
 
-template <typename Int>
+template <bool HI = false, typename Int>
 __device__ __forceinline__ uint32_t decode_ints3(WordReader& r, const uint32_t* sq, Int (&q)[64], uint32_t budget,
                                                  uint32_t prec)
 {
   using S = typename std::conditional<sizeof(Int) == 4, float, double>::type;
   constexpr int PREC = Traits<S>::kIntPrec;
-  uint64_t P[PREC];
-  uint32_t used = decode_planes64<PREC>(r, sq, budget, prec, P);
-  if constexpr (PREC == 32)
-    coeffs_from_planes(q, P);
-  else
-    coeffs_from_planes(q, P, prec > 32);
-  return used;
+  if constexpr (HI && PREC == 64) {
+    uint64_t P[32];
+    const uint32_t used = decode_planes64<32>(r, sq, budget, prec, P);
+    coeffs_from_planes_hi(q, P);
+    return used;
+  } else {
+    uint64_t P[PREC];
+    uint32_t used = decode_planes64<PREC>(r, sq, budget, prec, P);
+    if constexpr (PREC == 32)
+      coeffs_from_planes(q, P);
+    else
+      coeffs_from_planes(q, P, prec > 32);
+    return used;
+  }
 }
 
 // Block exponent and block-floating-point cast for the lossy encoder.  Fast
@@ -388,7 +440,7 @@ __device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], double (&v)[64]
 // Encode one block into a zeroed slot; returns its length in bits including
 // minbits padding (padding bits are the slot's zeros).  FR: fixed rate with
 // maxprec >= intprec (no per-block precision limit; see code_planes).
-template <typename S, bool REV, bool FR = false, typename Reload>
+template <typename S, bool REV, bool FR = false, bool HI = false, typename Reload>
 __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut, S (&v)[64], const CodecParams& cp,
                                                   Reload&& reload)
 {
@@ -445,7 +497,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
     if (prec > cp.maxprec) prec = cp.maxprec;
     if (prec < 1) prec = 1;
     w.put32(bits, prec - 1);
-    const uint32_t end = encode_ints3<true>(w, lut, q, bits + T::kPbits, cp.maxbits, prec);
+    const uint32_t end = encode_ints3<true, HI>(w, lut, q, bits + T::kPbits, cp.maxbits, prec);
     uint32_t ib = end - bits;
     if (ib < minb) ib = minb;
     return bits + ib;
@@ -460,7 +512,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
       bits += kE;
       xform<3, false, false>(q);
       const uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
-      uint32_t ib = encode_ints3<!FR>(w, lut, q, bits, cp.maxbits, mp) - bits;
+      uint32_t ib = encode_ints3<!FR, HI>(w, lut, q, bits, cp.maxbits, mp) - bits;
       if (ib < minb) ib = minb;
       bits += ib;
     } else if (cp.minbits > bits) {
@@ -471,7 +523,7 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
 }
 
 // Decode one block; returns the number of bits consumed (incl. padding).
-template <typename S, bool REV>
+template <typename S, bool REV, bool HI = false>
 __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t* sq, S (&v)[64], const CodecParams& cp)
 {
   using T = Traits<S>;
@@ -500,7 +552,7 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t*
     uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
     uint32_t maxb = cp.maxbits - bits;
     uint32_t prec = (uint32_t)r.read(T::kPbits) + 1;
-    uint32_t ib = T::kPbits + decode_ints3(r, sq, q, maxb - T::kPbits, prec);
+    uint32_t ib = T::kPbits + decode_ints3<HI>(r, sq, q, maxb - T::kPbits, prec);
     if (ib < minb) {
       r.skip(minb - ib);
       ib = minb;
@@ -529,7 +581,7 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t*
     int emax = (int)r.read(kE) - T::kEbias;
     uint32_t mp = precision3(emax, cp);
     uint32_t minb = cp.minbits - (bits < cp.minbits ? bits : cp.minbits);
-    uint32_t ib = decode_ints3(r, sq, q, cp.maxbits - bits, mp);
+    uint32_t ib = decode_ints3<HI>(r, sq, q, cp.maxbits - bits, mp);
     if (ib < minb) {
       r.skip(minb - ib);
       ib = minb;

@@ -203,7 +203,8 @@ template <int NB>
 __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
                                           const uint32_t* wrt, uint64_t w, uint64_t start, uint32_t total);
 
-template <typename S, bool VEC, bool REV>
+// HI: double with maxprec <= 32 (planes 32..63 only, block3.h encode_ints3)
+template <typename S, bool VEC, bool REV, bool HI = false>
 __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        GeneralArgs a)
 {
@@ -237,7 +238,7 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
     OrSlot os{wbase + (size_t)lane * a.swp, 2 * a.swp - 1};
-    len = encode_block3<S, REV>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
+    len = encode_block3<S, REV, false, HI>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
   const uint32_t incl = wave_incl_scan(len);
   const uint32_t excl_l = incl - len;
@@ -374,7 +375,7 @@ struct DecodeArgs {
 // the same offset of their blocks hit different banks), funnel-shifted so the
 // block starts at bit 0.  Staging is cooperative: thread t copies word j of
 // block l for t = l*W + j, so consecutive threads read consecutive stream words.
-template <typename S, bool VEC, bool REV>
+template <typename S, bool VEC, bool REV, bool HI = false>
 __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
 {
   __shared__ uint32_t sq[256];
@@ -426,7 +427,7 @@ __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g,
   r.w = wslot + (size_t)lane * a.swp;
   r.pos = 0;
   S v[64];
-  decode_block3<S, REV>(r, sq, v, cp);
+  decode_block3<S, REV, HI>(r, sq, v, cp);
   BlockPos p = block_pos(g, b, 3);
   scatter3<S, VEC>(v, data, g, p);
 }

@@ -222,6 +222,42 @@ static size_t slot_words_odd(uint32_t bits)
 // ---------------------------------------------------------------------------
 // launchers
 
+// double with maxprec <= 32: the kernels that code planes 32..63 only
+template <typename S>
+static bool hi_planes(const Plan& p)
+{
+  return sizeof(S) == 8 && p.cp.maxprec <= 32;
+}
+
+template <typename S, bool HI>
+static void launch_general3(Ctx* c, const Plan& p, const S* d_field, dim3 grid, dim3 block, size_t lds,
+                            const GeneralArgs& a)
+{
+  const bool rev = p.cp.minexp < kMinExp;
+  if (p.vec && rev)
+    hipLaunchKernelGGL((encode3_general<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (p.vec)
+    hipLaunchKernelGGL((encode3_general<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (rev)
+    hipLaunchKernelGGL((encode3_general<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else
+    hipLaunchKernelGGL((encode3_general<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+}
+
+template <typename S, bool HI>
+static void launch_decode3(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 block, size_t lds, const DecodeArgs& a)
+{
+  const bool rev = p.cp.minexp < kMinExp;
+  if (p.vec && rev)
+    hipLaunchKernelGGL((decode3<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (p.vec)
+    hipLaunchKernelGGL((decode3<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else if (rev)
+    hipLaunchKernelGGL((decode3<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  else
+    hipLaunchKernelGGL((decode3<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+}
+
 // Arguments of the packing encoders (encode3_general, encode4) for `nwaves`
 // waves: fix-up partials, look-back state and, for a variable-rate stream with
 // an index, the index buffers.  Queues the look-back resets on the stream.
@@ -381,15 +417,14 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   if (!general_args(c, p, nwaves, swp, d_out, g0, index, a))
     return 0;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  const bool rev = p.cp.minexp < kMinExp;
-  if (p.vec && rev)
-    hipLaunchKernelGGL((encode3_general<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (p.vec)
-    hipLaunchKernelGGL((encode3_general<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (rev)
-    hipLaunchKernelGGL((encode3_general<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else
-    hipLaunchKernelGGL((encode3_general<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  if constexpr (sizeof(S) == 8) {
+    if (hi_planes<S>(p))
+      launch_general3<S, true>(c, p, d_field, grid, block, lds, a);
+    else
+      launch_general3<S, false>(c, p, d_field, grid, block, lds, a);
+  } else {
+    launch_general3<S, false>(c, p, d_field, grid, block, lds, a);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   return finish_general(c, p, nwaves, d_out, g0, head_word, a, index, total_bits);
@@ -471,15 +506,14 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
     return fail("zfp_hip: block size too large for LDS staging (%u bits)", per_block);
   dim3 grid((unsigned)ngroups), block(256);
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  const bool rev = p.cp.minexp < kMinExp;
-  if (p.vec && rev)
-    hipLaunchKernelGGL((decode3<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (p.vec)
-    hipLaunchKernelGGL((decode3<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (rev)
-    hipLaunchKernelGGL((decode3<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else
-    hipLaunchKernelGGL((decode3<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  if constexpr (sizeof(S) == 8) {
+    if (hi_planes<S>(p))
+      launch_decode3<S, true>(c, p, d_field, grid, block, lds, a);
+    else
+      launch_decode3<S, false>(c, p, d_field, grid, block, lds, a);
+  } else {
+    launch_decode3<S, false>(c, p, d_field, grid, block, lds, a);
+  }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   return 1;

@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--decode", action="store_true")
     ap.add_argument("--dims", type=int, default=3)
+    ap.add_argument("--host", action="store_true", help="field and stream in host memory (PCIe-inclusive)")
     a = ap.parse_args()
     import torch
     from capi import ZfpCAPI
@@ -63,11 +64,21 @@ def main():
     else:
         f = field(torch, a.n, dt, dev)
         zf = lib.zfp_field_3d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.n)
+    if a.host:  # pinned? no: plain pageable numpy arrays, as a zfpy caller hands them over
+        f = f.cpu().numpy()
+        shape = [a.n] * a.dims
+        fn = lib.zfp_field_4d if a.dims == 4 else lib.zfp_field_3d
+        zf = fn(ctypes.c_void_p(f.ctypes.data), zt, *shape)
     zs = lib.zfp_stream_open(None)
     api.set_mode(zs, a.mode, a.param if a.mode != "reversible" else None, zt, a.dims)
     cap = lib.zfp_stream_maximum_size(zs, zf)
-    out = torch.zeros(cap, dtype=torch.uint8, device=dev)
-    bs = lib.stream_open(ctypes.c_void_p(out.data_ptr()), cap)
+    if a.host:
+        import numpy as np
+        out_np = np.zeros(cap, dtype=np.uint8)
+        bs = lib.stream_open(ctypes.c_void_p(out_np.ctypes.data), cap)
+    else:
+        out = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        bs = lib.stream_open(ctypes.c_void_p(out.data_ptr()), cap)
     lib.zfp_stream_set_bit_stream(zs, bs)
     ks = []
     for i in range(a.iters):
@@ -76,21 +87,26 @@ def main():
         assert nb, lib.zfp_hip_last_error()
         k, t = ctypes.c_double(), ctypes.c_double()
         lib.zfp_hip_last_timing(ctypes.byref(k), ctypes.byref(t))
-        ks.append(k.value)
-    gb = f.numel() * f.element_size() / 1e9
-    print("encode %dD %s %s %s: bytes=%d kernel_ms=%s  GB/s=%.1f" % (a.dims, a.dtype, a.mode, a.param, nb,
+        ks.append(t.value if a.host else k.value)
+    gb = (f.nbytes if a.host else f.numel() * f.element_size()) / 1e9
+    print(("host->host call " if a.host else "") + "encode %dD %s %s %s: bytes=%d kernel_ms=%s  GB/s=%.1f" % (a.dims, a.dtype, a.mode, a.param, nb,
           " ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
     if a.decode:
-        back = torch.empty_like(f)
-        lib.zfp_field_set_pointer(zf, ctypes.c_void_p(back.data_ptr()))
+        if a.host:
+            import numpy as np
+            back = np.empty_like(f)
+            lib.zfp_field_set_pointer(zf, ctypes.c_void_p(back.ctypes.data))
+        else:
+            back = torch.empty_like(f)
+            lib.zfp_field_set_pointer(zf, ctypes.c_void_p(back.data_ptr()))
         ks = []
         for i in range(a.iters):
             lib.stream_rewind(bs)
             assert lib.zfp_decompress(zs, zf), lib.zfp_hip_last_error()
             k, t = ctypes.c_double(), ctypes.c_double()
             lib.zfp_hip_last_timing(ctypes.byref(k), ctypes.byref(t))
-            ks.append(k.value)
-        print("decode kernel_ms=%s  GB/s=%.1f" % (" ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
+            ks.append(t.value if a.host else k.value)
+        print(("host->host call " if a.host else "") + "decode kernel_ms=%s  GB/s=%.1f" % (" ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
 
 
 if __name__ == "__main__":

@@ -21,7 +21,7 @@ int main()
     int dens = it % 4;
     if (dens) for (int k = 0; k < dens; k++) w[0] &= rng(), w[1] &= rng();
     uint32_t n0 = (uint32_t)(rng() % 65), bits0 = (uint32_t)(rng() % 300) + 1;
-    uint64_t pos0 = rng() % 64;
+    uint32_t pos0 = (uint32_t)(rng() % 64);
     WordReader a{w, pos0}, b{w, pos0};
     uint32_t na = n0, nb = n0, ba = bits0, bb = bits0;
     uint64_t xa = decode_plane64(a, sq, ba, na);

@@ -163,17 +163,17 @@ __device__ __forceinline__ uint32_t dbl16(const uint32_t* lut, uint32_t u)
 // Bit reader over a word array in LDS (or global memory).
 struct WordReader {
   const uint64_t* w;
-  uint64_t pos;
+  uint32_t pos;  // bit position within the lane's slot (slots are small)
 
-  __device__ __forceinline__ uint64_t peek64() const
+  // Branch-free 64-bit window at bit p: both words are always read (the slot
+  // has a spare word past its last), and (b << 1) << (63 - s) vanishes at s = 0.
+  __device__ __forceinline__ uint64_t peek_at(uint32_t p) const
   {
-    uint64_t i = pos >> 6;
-    uint32_t r = (uint32_t)(pos & 63);
-    uint64_t v = w[i] >> r;
-    if (r)
-      v |= w[i + 1] << (64 - r);
-    return v;
+    const uint32_t i = p >> 6, s = p & 63u;
+    const uint64_t a = w[i], b = w[i + 1];
+    return (a >> s) | ((b << 1) << (63u - s));
   }
+  __device__ __forceinline__ uint64_t peek64() const { return peek_at(pos); }
   __device__ __forceinline__ uint64_t read(uint32_t n)
   {
     uint64_t v = n ? (peek64() & low_mask(n)) : 0ull;
@@ -182,12 +182,11 @@ struct WordReader {
   }
   __device__ __forceinline__ uint32_t read1()
   {
-    uint64_t i = pos >> 6;
-    uint32_t r = (uint32_t)(pos & 63);
+    const uint32_t i = pos >> 6, s = pos & 63u;
     pos++;
-    return (uint32_t)((w[i] >> r) & 1u);
+    return (uint32_t)((w[i] >> s) & 1u);
   }
-  __device__ __forceinline__ void skip(uint64_t n) { pos += n; }
+  __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
 };
 
 // ---------------------------------------------------------------------------
@@ -642,49 +641,62 @@ __device__ __forceinline__ void decode_group_slow(WordReader& r, uint64_t& x, ui
   }
 }
 
+// Squeeze of a mask F of pair-first bits (each one is followed by its pair's
+// deleted second bit): the r-th one, at bit p, moves to bit p - r.  Eight byte
+// look-ups merged pairwise in 32-bit halves -- no loop, no 64-bit shift per
+// byte; the length of a squeezed piece is its bit width minus its ones.
+__device__ __forceinline__ uint32_t squeeze32(const uint32_t* sq, uint32_t f)
+{
+  const uint32_t b0 = f & 0xffu, b1 = (f >> 8) & 0xffu, b2 = (f >> 16) & 0xffu, b3 = f >> 24;
+  const uint32_t u0 = sq[b0] | (sq[b1] << (8u - (uint32_t)__popc(b0)));
+  const uint32_t u1 = sq[b2] | (sq[b3] << (8u - (uint32_t)__popc(b2)));
+  return u0 | (u1 << (16u - (uint32_t)__popc(f & 0xffffu)));
+}
+
+__device__ __forceinline__ uint64_t squeeze64(const uint32_t* sq, uint64_t F)
+{
+  const uint32_t lo = (uint32_t)F, hi = (uint32_t)(F >> 32);
+  return (uint64_t)squeeze32(sq, lo) | ((uint64_t)squeeze32(sq, hi) << (32u - (uint32_t)__popc(lo)));
+}
+
+// One bit plane: n verbatim bits, then the group section.  Straight-line for
+// every lane (the verbatim window and the section window are both read, the
+// section is parsed in closed form and its consumption selected); only lanes
+// whose section is not closed-form run the reference loop, in a wave-uniform
+// branch.
 __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
 {
-  uint32_t m = n < bits ? n : bits;
-  uint64_t x = r.read(m);
-  bits -= m;
-  bool slow = false;
-  if (n < 64 && bits) {
-    const uint64_t w = r.peek64();
-    if (!(w & 1)) {
-      r.skip(1);
-      bits--;
-    } else {
-      const uint64_t S = w >> 1;
-      const uint64_t starts = S & ~(S << 1);
-      const uint64_t se = S + (starts & kEven), so = S + (starts & kOdd);
-      // S holds 63 stream bits; its bit 63 is not data, so a run reaching
-      // bit 62 must not be taken as ended there
-      const uint64_t ends = (((se & ~S) & kOdd) | ((so & ~S) & kEven)) & ~(1ull << 63);
-      const uint32_t q = ctz64(ends);
-      const uint64_t mq = low_mask(q);
-      const uint32_t ones = (uint32_t)__popcll(S & mq);
-      const uint32_t P = q - (ones - 1) / 2;
-      if (ends != 0 && n + P <= 63 && q + 2 <= bits) {
-        uint64_t F = S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd));
-        uint64_t xx = 0;
-        uint32_t sh = 0;
-        while (__any(F != 0)) {
-          const uint32_t b = (uint32_t)F & 0xffu;
-          xx |= (uint64_t)sq[b] << sh;
-          sh += 8u - (uint32_t)__popc(b);
-          F >>= 8;
-        }
-        x |= xx << n;
-        n += P;
-        r.skip(q + 2);
-        bits -= q + 2;
-      } else {
-        slow = true;
-      }
-    }
+  const uint32_t m = n < bits ? n : bits;
+  uint32_t pos = r.pos;
+  const uint64_t V = r.peek_at(pos);
+  uint64_t x = m ? V & (~0ull >> ((64u - m) & 63u)) : 0ull;
+  pos += m;
+  uint32_t bl = bits - m;
+  const bool grp = n < 64 && bl != 0;
+  const uint64_t w = r.peek_at(pos);
+  const bool one = (w & 1) != 0;
+  const uint64_t S = w >> 1;
+  const uint64_t starts = S & ~(S << 1);
+  const uint64_t se = S + (starts & kEven), so = S + (starts & kOdd);
+  // S holds 63 stream bits; its bit 63 is not data, so a run reaching
+  // bit 62 must not be taken as ended there
+  const uint64_t ends = (((se & ~S) & kOdd) | ((so & ~S) & kEven)) & ~(1ull << 63);
+  const uint32_t q = ctz64(ends);
+  const uint64_t mq = low_mask(q);
+  const uint32_t ones = (uint32_t)__popcll(S & mq);
+  const uint32_t P = q - (ones - 1) / 2;
+  const bool fast = grp && one && ends != 0 && n + P <= 63 && q + 2 <= bl;
+  const uint64_t F = S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd));
+  x |= squeeze64(sq, fast ? F : 0ull) << (n & 63u);
+  const uint32_t used = fast ? q + 2u : (grp && !one ? 1u : 0u);
+  n = fast ? n + P : n;
+  r.pos = pos + used;
+  bits = bl - used;
+  const bool slow = grp && one && !fast;
+  if (__any(slow)) {
+    if (slow)
+      decode_group_slow(r, x, bits, n);
   }
-  if (slow)
-    decode_group_slow(r, x, bits, n);
   return x;
 }
 
@@ -693,11 +705,13 @@ struct DecodePlanes {
   static __device__ __forceinline__ void run(WordReader& r, const uint32_t* sq, uint64_t (&P)[PREC], uint32_t kmin,
                                              uint32_t& bits, uint32_t& n)
   {
-    bool act = bits != 0 && (uint32_t)K >= kmin;
+    const bool act = bits != 0 && (uint32_t)K >= kmin;
     if (!__any(act))
       return;
-    if (act)
-      P[K] = decode_plane64(r, sq, bits, n);
+    // a lane past its precision limit decodes with no budget: no effect
+    uint32_t b = act ? bits : 0u;
+    P[K] = decode_plane64(r, sq, b, n);
+    bits = act ? b : bits;
     DecodePlanes<K - 1, PREC>::run(r, sq, P, kmin, bits, n);
   }
 };

@@ -653,12 +653,6 @@ __device__ __forceinline__ uint32_t squeeze32(const uint32_t* sq, uint32_t f)
   return u0 | (u1 << (16u - (uint32_t)__popc(f & 0xffffu)));
 }
 
-__device__ __forceinline__ uint64_t squeeze64(const uint32_t* sq, uint64_t F)
-{
-  const uint32_t lo = (uint32_t)F, hi = (uint32_t)(F >> 32);
-  return (uint64_t)squeeze32(sq, lo) | ((uint64_t)squeeze32(sq, hi) << (32u - (uint32_t)__popc(lo)));
-}
-
 // One bit plane: n verbatim bits, then the group section.  Straight-line for
 // every lane (the verbatim window and the section window are both read, the
 // section is parsed in closed form and its consumption selected); only lanes
@@ -673,6 +667,11 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   pos += m;
   uint32_t bl = bits - m;
   const bool grp = n < 64 && bl != 0;
+  if (!__any(grp)) {  // every lane's plane is all verbatim (n == 64) or out of budget
+    r.pos = pos;
+    bits = bl;
+    return x;
+  }
   const uint64_t w = r.peek_at(pos);
   const bool one = (w & 1) != 0;
   const uint64_t S = w >> 1;
@@ -686,8 +685,12 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   const uint32_t ones = (uint32_t)__popcll(S & mq);
   const uint32_t P = q - (ones - 1) / 2;
   const bool fast = grp && one && ends != 0 && n + P <= 63 && q + 2 <= bl;
-  const uint64_t F = S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd));
-  x |= squeeze64(sq, fast ? F : 0ull) << (n & 63u);
+  const uint64_t F = fast ? S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd)) : 0ull;
+  const uint32_t Fl = (uint32_t)F, Fh = (uint32_t)(F >> 32);
+  uint64_t xx = squeeze32(sq, Fl);
+  if (__any(Fh != 0))  // some section reaches past stream bit 32
+    xx |= (uint64_t)squeeze32(sq, Fh) << (32u - (uint32_t)__popc(Fl));
+  x |= xx << (n & 63u);
   const uint32_t used = fast ? q + 2u : (grp && !one ? 1u : 0u);
   n = fast ? n + P : n;
   r.pos = pos + used;

@@ -341,11 +341,13 @@ struct Lift {
   }
   static __device__ __forceinline__ void inv(Int& x, Int& y, Int& z, Int& w)
   {
+    // decode.c:9-34.  Each "a += b; b <<= 1; b -= a" is, in wrapping
+    // arithmetic, b' = 2b - (a + b) = b - a and a' = a + b: two operations.
     y = add(y, w >> 1); w = sub(w, y >> 1);
-    y = add(y, w); w = shl1(w); w = sub(w, y);
-    z = add(z, x); x = shl1(x); x = sub(x, z);
-    y = add(y, z); z = shl1(z); z = sub(z, y);
-    w = add(w, x); x = shl1(x); x = sub(x, w);
+    Int t = y; y = add(y, w); w = sub(w, t);
+    t = z; z = add(z, x); x = sub(x, t);
+    t = y; y = add(y, z); z = sub(z, t);
+    t = w; w = add(w, x); x = sub(x, t);
   }
   static __device__ __forceinline__ void rfwd(Int& x, Int& y, Int& z, Int& w)
   {
@@ -681,7 +683,7 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   // bit 62 must not be taken as ended there
   const uint64_t ends = (((se & ~S) & kOdd) | ((so & ~S) & kEven)) & ~(1ull << 63);
   const uint32_t q = ctz64(ends);
-  const uint64_t mq = low_mask(q);
+  const uint64_t mq = (ends - 1) & ~ends;  // bits below q (all when ends == 0)
   const uint32_t ones = (uint32_t)__popcll(S & mq);
   const uint32_t P = q - (ones - 1) / 2;
   const bool fast = grp && one && ends != 0 && n + P <= 63 && q + 2 <= bl;

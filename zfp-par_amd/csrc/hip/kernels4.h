@@ -148,6 +148,16 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
   const uint64_t left = g.nblocks - first;
   const uint32_t nb = left < kBlocks4PerWave ? (uint32_t)left : kBlocks4PerWave;
   const uint32_t pairs = nb * a.W;
+  if (!a.var && (G & 63) == 0 && (a.maxbits & 63) == 0) {
+    // word-aligned fixed rate (wave-uniform): block l starts at word l * bw
+    const uint32_t bw = a.maxbits >> 6;
+    for (uint32_t t = lane; t < pairs; t += 64) {
+      const uint32_t l = __umulhi(t, a.wmagic);
+      const uint32_t j = t - l * a.W;
+      const uint64_t gw = W0 + l * bw + j;
+      region[l * a.swp + j] = gw < a.in_words ? a.in[gw] : 0ull;
+    }
+  } else
   for (uint32_t t = lane; t < pairs; t += 64) {
     const uint32_t l = __umulhi(t, a.wmagic);
     const uint32_t j = t - l * a.W;

@@ -687,17 +687,26 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   const uint32_t ones = (uint32_t)__popcll(S & mq);
   const uint32_t P = q - (ones - 1) / 2;
   const bool fast = grp && one && ends != 0 && n + P <= 63 && q + 2 <= bl;
-  const uint64_t F = fast ? S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd)) : 0ull;
+  // The section reaches coefficient 63 before its stop (or runs past the
+  // window): the reference parses the k63 = 63 - n tokens below it and sets
+  // bit 63 without reading it (decode.c:69-120, n < size - 1).  In the
+  // squeezed (token) domain a token costs 1 bit plus 1 if it is a one.
+  const bool imp0 = grp && one && !fast && (ends == 0 || n + P > 63);
+  const uint64_t F = (fast || imp0) ? S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd)) : 0ull;
   const uint32_t Fl = (uint32_t)F, Fh = (uint32_t)(F >> 32);
   uint64_t xx = squeeze32(sq, Fl);
   if (__any(Fh != 0))  // some section reaches past stream bit 32
     xx |= (uint64_t)squeeze32(sq, Fh) << (32u - (uint32_t)__popc(Fl));
-  x |= xx << (n & 63u);
-  const uint32_t used = fast ? q + 2u : (grp && !one ? 1u : 0u);
-  n = fast ? n + P : n;
+  const uint32_t k63 = (63u - n) & 63u;
+  const uint64_t xi = xx & ((1ull << k63) - 1);
+  const uint32_t si = k63 + (uint32_t)__popcll(xi);  // section bits of those tokens
+  const bool imp = imp0 && si <= 63u && si + 1u <= bl;
+  x |= (fast ? xx : (imp ? xi | (1ull << k63) : 0ull)) << (n & 63u);
+  const uint32_t used = fast ? q + 2u : (imp ? si + 1u : (grp && !one ? 1u : 0u));
+  n = fast ? n + P : (imp ? 64u : n);
   r.pos = pos + used;
   bits = bl - used;
-  const bool slow = grp && one && !fast;
+  const bool slow = grp && one && !fast && !imp;
   if (__any(slow)) {
     if (slow)
       decode_group_slow(r, x, bits, n);

@@ -373,7 +373,7 @@ __device__ __forceinline__ uint32_t decode_ints3(WordReader& r, const uint32_t* 
   constexpr int PREC = Traits<S>::kIntPrec;
   if constexpr (HI && PREC == 64) {
     uint64_t P[32];
-    const uint32_t used = decode_planes64<32>(r, sq, budget, prec, P);
+    const uint32_t used = decode_planes64<32, false>(r, sq, budget, prec, P);
     coeffs_from_planes_hi(q, P);
     return used;
   } else {

@@ -660,6 +660,7 @@ __device__ __forceinline__ uint32_t squeeze32(const uint32_t* sq, uint32_t f)
 // section is parsed in closed form and its consumption selected); only lanes
 // whose section is not closed-form run the reference loop, in a wave-uniform
 // branch.
+template <bool IMP = true>
 __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
 {
   const uint32_t m = n < bits ? n : bits;
@@ -691,16 +692,21 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   // window): the reference parses the k63 = 63 - n tokens below it and sets
   // bit 63 without reading it (decode.c:69-120, n < size - 1).  In the
   // squeezed (token) domain a token costs 1 bit plus 1 if it is a one.
-  const bool imp0 = grp && one && !fast && (ends == 0 || n + P > 63);
+  const bool imp0 = IMP && grp && one && !fast && (ends == 0 || n + P > 63);
   const uint64_t F = (fast || imp0) ? S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd)) : 0ull;
   const uint32_t Fl = (uint32_t)F, Fh = (uint32_t)(F >> 32);
   uint64_t xx = squeeze32(sq, Fl);
   if (__any(Fh != 0))  // some section reaches past stream bit 32
     xx |= (uint64_t)squeeze32(sq, Fh) << (32u - (uint32_t)__popc(Fl));
-  const uint32_t k63 = (63u - n) & 63u;
-  const uint64_t xi = xx & ((1ull << k63) - 1);
-  const uint32_t si = k63 + (uint32_t)__popcll(xi);  // section bits of those tokens
-  const bool imp = imp0 && si <= 63u && si + 1u <= bl;
+  uint32_t k63 = 0, si = 0;
+  uint64_t xi = 0;
+  bool imp = false;
+  if (__any(imp0)) {  // wave-uniform: most planes have no such lane
+    k63 = (63u - n) & 63u;
+    xi = xx & ((1ull << k63) - 1);
+    si = k63 + (uint32_t)__popcll(xi);  // section bits of those tokens
+    imp = imp0 && si <= 63u && si + 1u <= bl;
+  }
   x |= (fast ? xx : (imp ? xi | (1ull << k63) : 0ull)) << (n & 63u);
   const uint32_t used = fast ? q + 2u : (imp ? si + 1u : (grp && !one ? 1u : 0u));
   n = fast ? n + P : (imp ? 64u : n);
@@ -714,7 +720,7 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   return x;
 }
 
-template <int K, int PREC>
+template <int K, int PREC, bool IMP>
 struct DecodePlanes {
   static __device__ __forceinline__ void run(WordReader& r, const uint32_t* sq, uint64_t (&P)[PREC], uint32_t kmin,
                                              uint32_t& bits, uint32_t& n)
@@ -724,21 +730,23 @@ struct DecodePlanes {
       return;
     // a lane past its precision limit decodes with no budget: no effect
     uint32_t b = act ? bits : 0u;
-    P[K] = decode_plane64(r, sq, b, n);
+    P[K] = decode_plane64<IMP>(r, sq, b, n);
     bits = act ? b : bits;
-    DecodePlanes<K - 1, PREC>::run(r, sq, P, kmin, bits, n);
+    DecodePlanes<K - 1, PREC, IMP>::run(r, sq, P, kmin, bits, n);
   }
 };
 
-template <int PREC>
-struct DecodePlanes<-1, PREC> {
+template <int PREC, bool IMP>
+struct DecodePlanes<-1, PREC, IMP> {
   static __device__ __forceinline__ void run(WordReader&, const uint32_t*, uint64_t (&)[PREC], uint32_t, uint32_t&,
                                              uint32_t&)
   {
   }
 };
 
-template <int PREC>
+// IMP: closed form for sections reaching coefficient 63 (false for the f64
+// maxprec <= 32 decoder, where it measured slower than the reference loop).
+template <int PREC, bool IMP = true>
 __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_t* sq, uint32_t budget,
                                                     uint32_t maxprec, uint64_t (&P)[PREC])
 {
@@ -748,7 +756,7 @@ __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_
 #pragma unroll
   for (int k = 0; k < PREC; k++)
     P[k] = 0;
-  DecodePlanes<PREC - 1, PREC>::run(r, sq, P, kmin, bits, n);
+  DecodePlanes<PREC - 1, PREC, IMP>::run(r, sq, P, kmin, bits, n);
   return budget - bits;
 }
 

@@ -16,8 +16,13 @@
  *                       decompress_strided_<T>_3/_4 (src/template/decompress.c:66-140)
  *                       with the decoders of src/template/{decodef,decode,...}.c
  *   zfp_hip_index_*     no reference equivalent: variable-rate streams carry no
- *                       block offsets (docs execution.rst), so the GPU encoder
- *                       emits a side-band block index that the GPU decoder uses.
+ *                       block offsets (docs execution.rst).  The GPU encoder can
+ *                       emit a side-band block index; without one (a stream
+ *                       from the reference, a file, another process) the
+ *                       decoder first finds the block starts with a parallel
+ *                       resynchronising parse of the stream (zfp_hip_index_build),
+ *                       which replaces the serial block walk of
+ *                       src/template/decompress.c:66-140.
  *
  * Memory: `field_base` and `words` may each be host or device (hipMalloc)
  * memory; the library stages host buffers through device memory itself.
@@ -74,12 +79,22 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
 /*
  * Decode the chunk box of `job` from the stream at `words` (readable capacity
  * `capacity_words`), starting at bit `bit_offset`; *end_bit receives the bit
- * position after the last block.  Variable-rate modes need the `index` made
- * by zfp_hip_compress for this stream.
+ * position after the last block.  For variable-rate modes `index` is used when
+ * it was made for this block count, layout and bit offset (zfp_hip_compress or
+ * zfp_hip_index_build); otherwise (or when NULL) the stream is scanned first.
  */
 int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t* words,
                        uint64_t capacity_words, uint64_t bit_offset, int device,
                        const zfp_hip_index* index, uint64_t* end_bit);
+
+/*
+ * Build the block index of the variable-rate stream at `words` for the chunk
+ * box of `job`, blocks starting at bit `bit_offset` (a parallel parse of the
+ * stream on the GPU; see scan.h).  Returns 0 for fixed-rate jobs, truncated
+ * streams or HIP errors.
+ */
+int zfp_hip_index_build(const zfp_hip_job* job, const uint64_t* words, uint64_t capacity_words,
+                        uint64_t bit_offset, int device, zfp_hip_index* index);
 
 /* Block index (variable-rate streams). */
 zfp_hip_index* zfp_hip_index_create(void);
@@ -96,6 +111,20 @@ zfp_hip_index* zfp_hip_index_import(const void* buffer, size_t bytes);
  * call (staging copies, fix-ups, kernel).  Returns 0 if no call has run.
  */
 int zfp_hip_last_timing(double* kernel_ms, double* total_ms);
+
+/* Index scan of the most recent call on this thread (decompress without a
+ * matching index, or zfp_hip_index_build): its duration from HIP events and
+ * the number of segment passes.  Returns 0 if that call did not scan. */
+int zfp_hip_last_scan(double* scan_ms, int* passes);
+
+/*
+ * Device scratch: calls borrow a context (HIP stream + reusable buffers) from
+ * a process-wide pool, so scratch is bounded by the peak number of concurrent
+ * calls.  zfp_hip_scratch_bytes() reports what idle contexts hold;
+ * zfp_hip_release_scratch() frees them (returns how many were freed).
+ */
+size_t zfp_hip_scratch_bytes(void);
+int zfp_hip_release_scratch(void);
 
 #ifdef __cplusplus
 }

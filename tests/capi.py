@@ -147,7 +147,9 @@ class ZfpCAPI:
         """Product library only: bind the MI355X block-index extension."""
         for name, res, args in [("zfp_stream_hip_index", vp, [vp]), ("zfp_stream_set_hip_index", i32, [vp, vp]),
                                 ("zfp_hip_index_free", None, [vp]), ("zfp_hip_device_count", i32, []),
-                                ("zfp_hip_last_timing", i32, [vp, vp]), ("zfp_hip_last_error", ctypes.c_char_p, [])]:
+                                ("zfp_hip_last_timing", i32, [vp, vp]), ("zfp_hip_last_error", ctypes.c_char_p, []),
+                                ("zfp_hip_last_scan", i32, [vp, vp]), ("zfp_hip_scratch_bytes", sz, []),
+                                ("zfp_hip_release_scratch", i32, [])]:
             fn = getattr(self.lib, name)
             fn.restype = res
             fn.argtypes = args
@@ -215,6 +217,13 @@ class ZfpCAPI:
         self.lib.zfp_stream_close(zs)
         self.lib.zfp_field_free(field)
         return out, n
+
+    def last_scan(self):
+        """(ms, passes) of the index scan of the last decompress on this thread, or None."""
+        ms, passes = ctypes.c_double(), ctypes.c_int()
+        if not self.lib.zfp_hip_last_scan(ctypes.byref(ms), ctypes.byref(passes)):
+            return None
+        return ms.value, passes.value
 
     def make_chunk(self, ndim, box):
         """box: list of (f, e) per zfp axis (x first)."""

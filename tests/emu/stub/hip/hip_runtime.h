@@ -56,3 +56,13 @@ using std::fabs;
 #include <algorithm>
 using std::max;
 using std::min;
+// plain read-modify-write: the scan emulation runs lanes one after another
+static inline uint32_t atomicAdd(uint32_t* p, uint32_t v) { uint32_t o = *p; *p = o + v; return o; }
+// kernel built-ins, so headers that define kernels compile (the emulations
+// call the per-lane device functions, not the kernels)
+// (quad_emu.cpp brings its own per-thread threadIdx and barrier)
+#ifdef EMU_KERNEL_BUILTINS
+struct emu_dim3 { uint32_t x = 0, y = 0, z = 0; };
+inline emu_dim3 threadIdx, blockIdx, blockDim;
+static inline void __syncthreads() {}
+#endif

@@ -63,3 +63,14 @@ def test_4d_quad_codec_matches_oracle_all_modes(oracle_obj):
     r = subprocess.run([_build(d, "quad_emu.cpp", [obj, "-pthread"])], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert r.stdout.count(" 0/200 bad") == 32, r.stdout
+
+
+def test_index_scan_matches_oracle_block_starts(oracle_obj):
+    """scan.h (index-free variable-rate decode): per-block bit lengths and the
+    resynchronising segment passes recover every block start of oracle streams
+    in precision, accuracy, reversible and expert modes, 3D and 4D, f32 and f64,
+    at several segment sizes and unaligned stream offsets."""
+    d, obj = oracle_obj
+    r = subprocess.run([_build(d, "scan_emu.cpp", [obj])], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "scan mismatches 0" in r.stdout, r.stdout

@@ -1,0 +1,437 @@
+// Block index of a variable-rate stream that carries none (any zfp stream in
+// precision, accuracy, reversible or expert mode -- the reference's serial
+// decoder finds block i only by decoding blocks 0..i-1: decompress.c:66-140,
+// decode.c:69-246, revdecode.c:34-52).
+//
+// Parallel resynchronising parse.  The stream is cut into segments of L bits,
+// one lane per segment:
+//
+//   pass 1  lane s parses blocks from the segment's first bit as if a block
+//           started there (speculatively: only segment 0 starts at a real
+//           block) until it leaves the segment, marking every block start in
+//           a bitmap (1 bit per stream bit) and recording where it left, X[s].
+//   pass k  lane s re-parses from X[s-1], the exit of the chain of segment
+//           s-1.  Parsing is deterministic, so the moment this chain lands on
+//           a start already marked in segment s it coincides with segment s's
+//           chain from there on: the lane rewrites the bits before that point
+//           and stops ("merged"; X[s] unchanged).  A chain that crosses the
+//           whole segment without merging replaces it and moves X[s], so
+//           segment s+1 is redone in the next pass.  Passes repeat until no
+//           exit moves; then segment 0's true chain runs through every
+//           segment, so the first nblocks+1 set bits are the block starts and
+//           the end of the last block.
+//
+// Invariant after every pass: each segment's bitmap holds exactly one parse
+// chain restricted to the segment, and X[s] is that chain's exit.
+//
+// The per-block parse is the decoder's bit consumption without the values:
+// header (decodef.c:7-36, revdecodef.c:22-59), minbits/maxbits (decode.c:
+// 271-287), and per plane the n verbatim bits plus the group-test section,
+// in closed form when the section ends inside a 64-bit window (the decoder's
+// carry trick, codec_dev.h) and by the reference loop otherwise.  A lane's
+// stream bits come through a per-lane LDS ring refilled from prefetched
+// registers, so global latency is paid once per 512 bits.
+#pragma once
+
+#include "codec_dev.h"
+
+namespace zfp_amd {
+
+// ---------------------------------------------------------------------------
+// per-lane stream reader: ring of kRing words in LDS + kHalf prefetched words
+constexpr uint32_t kRing = 16;
+constexpr uint32_t kHalf = kRing / 2;
+
+struct RingReader {
+  const uint64_t* in;   // stream words (word 0 holds relative bit -g0 .. )
+  uint64_t in_words;
+  uint32_t g0;          // relative position r is absolute bit g0 + r of in[]
+  uint64_t* ring;       // kRing words (this lane's)
+  uint64_t base;        // absolute word index held in ring slot base % kRing
+  uint64_t nxt[kHalf];  // words [base + kRing, base + kRing + kHalf)
+
+  __device__ __forceinline__ uint64_t word(uint64_t i) const { return i < in_words ? in[i] : 0ull; }
+
+  __device__ __forceinline__ void fetch_next()
+  {
+#pragma unroll
+    for (uint32_t j = 0; j < kHalf; j++)
+      nxt[j] = word(base + kRing + j);
+  }
+  // fill the ring with the words from the one holding absolute word i
+  __device__ __forceinline__ void start_word(uint64_t i)
+  {
+    base = i & ~(uint64_t)(kHalf - 1);
+#pragma unroll
+    for (uint32_t j = 0; j < kRing; j++)
+      ring[(base + j) % kRing] = word(base + j);
+    fetch_next();
+  }
+  __device__ __forceinline__ void start(uint64_t rel) { start_word((g0 + rel) >> 6); }
+  // make words i and i+1 resident (i >= base: positions only move forward)
+  __device__ __forceinline__ void ensure(uint64_t i)
+  {
+    if (i + 1 < base + kRing)
+      return;
+    if (i + 1 >= base + kRing + kHalf) {  // jumped past the prefetched half
+      start_word(i);
+      return;
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kHalf; j++)
+      ring[(base + kRing + j) % kRing] = nxt[j];
+    base += kHalf;
+    fetch_next();
+  }
+  // 64 stream bits starting at relative bit r (LSB = bit r)
+  __device__ __forceinline__ uint64_t peek(uint64_t r)
+  {
+    const uint64_t a = g0 + r;
+    const uint64_t i = a >> 6;
+    const uint32_t s = (uint32_t)(a & 63);
+    ensure(i);
+    const uint64_t lo = ring[i % kRing], hi = ring[(i + 1) % kRing];
+    return s ? (lo >> s) | (hi << (64 - s)) : lo;
+  }
+};
+
+// ---------------------------------------------------------------------------
+// bit consumption of one block
+
+struct ScanParams {
+  uint32_t minbits, maxbits, maxprec;
+  int32_t minexp;
+};
+
+// Group-test section of one plane (decode.c:69-246 group loop) at bit p with
+// n < SIZE coefficients significant and bits > 0 budget.
+template <int SIZE, typename R>
+__device__ __forceinline__ void scan_section(R& rd, uint64_t& p, uint32_t& bits, uint32_t& n)
+{
+  const uint64_t w = rd.peek(p);
+  if (!(w & 1)) {  // "0": no one left in this plane
+    p++;
+    bits--;
+    return;
+  }
+  {
+    // closed form: after the "1" test the section is tokens "0", "11", "10"
+    // and ends at the first run of ones of odd length (codec_dev.h)
+    const uint64_t S = w >> 1;
+    const uint64_t starts = S & ~(S << 1);
+    const uint64_t se = S + (starts & kEven), so = S + (starts & kOdd);
+    const uint64_t ends = (((se & ~S) & kOdd) | ((so & ~S) & kEven)) & ~(1ull << 63);
+    if (ends) {
+      const uint32_t q = ctz64(ends);
+      const uint64_t mq = (ends - 1) & ~ends;
+      const uint32_t ones = (uint32_t)__popcll(S & mq);
+      const uint32_t P = q - (ones - 1) / 2;
+      if (n + P <= (uint32_t)SIZE - 1 && q + 2 <= bits) {
+        p += q + 2;
+        bits -= q + 2;
+        n += P;
+        return;
+      }
+    }
+  }
+  // reference loop (long sections, the implicit last coefficient, budget cuts)
+  while (bits && n < (uint32_t)SIZE) {
+    bits--;
+    const uint32_t t = (uint32_t)(rd.peek(p) & 1);
+    p++;
+    if (!t)
+      break;
+    uint32_t rem = (uint32_t)SIZE - 1 - n;
+    rem = rem < bits ? rem : bits;
+    for (;;) {
+      const uint32_t z = ctz64(rd.peek(p));
+      if (z < 64 && z < rem) {  // a one: the coefficient at n + z
+        p += z + 1;
+        bits -= z + 1;
+        n += z;
+        break;
+      }
+      if (rem <= 64) {  // all zeros up to the implicit coefficient or the budget
+        p += rem;
+        bits -= rem;
+        n += rem;
+        break;
+      }
+      p += 64;
+      bits -= 64;
+      n += 64;
+      rem -= 64;
+    }
+    n++;
+  }
+}
+
+// planes intprec-1 .. intprec-maxprec with `budget` bits: decode_ints
+template <int SIZE, int INTPREC, typename R>
+__device__ __forceinline__ uint32_t scan_planes(R& rd, uint64_t p, uint32_t budget, uint32_t maxprec)
+{
+  const uint32_t np = maxprec < (uint32_t)INTPREC ? maxprec : (uint32_t)INTPREC;
+  uint32_t bits = budget, n = 0;
+  for (uint32_t k = 0; k < np && bits; k++) {
+    const uint32_t m = n < bits ? n : bits;
+    p += m;
+    bits -= m;
+    if (n < (uint32_t)SIZE && bits)
+      scan_section<SIZE>(rd, p, bits, n);
+  }
+  return budget - bits;
+}
+
+// Length in bits of the block starting at p (decodef.c:7-36 / revdecodef.c:22-59)
+template <typename S, int DIMS, bool REV, typename R>
+__device__ __forceinline__ uint32_t scan_block(R& rd, uint64_t p, const ScanParams& sp)
+{
+  using T = Traits<S>;
+  constexpr int SIZE = 1 << (2 * DIMS);
+  constexpr uint32_t kE = T::kEbits, kP = T::kPbits;
+  const uint64_t h = rd.peek(p);
+  const uint32_t zero_len = sp.minbits > 1 ? sp.minbits : 1u;
+  if (!(h & 1))
+    return zero_len;
+  if constexpr (REV) {
+    const bool reinterp = (h >> 1) & 1;
+    const uint32_t bits = reinterp ? 2u : 2u + kE;
+    const uint32_t minb = sp.minbits - (bits < sp.minbits ? bits : sp.minbits);
+    const uint32_t maxb = sp.maxbits - bits;
+    const uint32_t prec = (uint32_t)((h >> bits) & ((1u << kP) - 1)) + 1;
+    uint32_t ib = kP + scan_planes<SIZE, T::kIntPrec>(rd, p + bits + kP, maxb - kP, prec);
+    if (ib < minb)
+      ib = minb;
+    return bits + ib;
+  } else {
+    const int emax = (int)((h >> 1) & ((1u << kE) - 1)) - T::kEbias;
+    int pr = emax - sp.minexp + 2 * DIMS + 2;
+    if (pr < 0)
+      pr = 0;
+    const uint32_t mp = (uint32_t)pr < sp.maxprec ? (uint32_t)pr : sp.maxprec;
+    const uint32_t bits = 1 + kE;
+    const uint32_t minb = sp.minbits - (bits < sp.minbits ? bits : sp.minbits);
+    uint32_t ib = scan_planes<SIZE, T::kIntPrec>(rd, p + bits, sp.maxbits - bits, mp);
+    if (ib < minb)
+      ib = minb;
+    return bits + ib;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// segment pass
+
+struct ScanArgs {
+  const uint64_t* in;
+  uint64_t in_words;
+  uint32_t g0;
+  uint32_t first;        // 1: pass 1 (bitmap is all zero; speculative starts)
+  uint64_t seg_bits;     // L, a multiple of 64
+  uint64_t nseg;
+  uint64_t limit;        // bits [0, limit) are scanned (limit = extent + 1)
+  uint64_t* bm;          // boundary bitmap, ceil(limit / 64) words
+  uint64_t* entry_used;  // per segment: the entry the current chain started at
+  const uint64_t* xsnap; // per segment: exits before this pass
+  uint64_t* x;           // per segment: exits after this pass
+  uint32_t* moved;       // count of exits that moved in this pass
+  ScanParams sp;
+};
+
+// One segment of a pass (one lane).
+template <typename S, int DIMS, bool REV>
+__device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint64_t* ring)
+{
+  const uint64_t lo = s * a.seg_bits;
+  if (lo >= a.limit)
+    return;
+  const uint64_t hi = lo + a.seg_bits < a.limit ? lo + a.seg_bits : a.limit;
+  uint64_t e;
+  if (s == 0)
+    e = 0;
+  else if (a.first)
+    e = lo;
+  else
+    e = a.xsnap[s - 1];
+  if (!a.first) {
+    if (e == a.entry_used[s])
+      return;  // this segment's chain already starts where the previous one exits
+  }
+  a.entry_used[s] = e;
+  RingReader rd;
+  rd.in = a.in;
+  rd.in_words = a.in_words;
+  rd.g0 = a.g0;
+  rd.ring = ring;
+  rd.start(e);
+  const bool check = !a.first;
+  const bool runs = a.sp.minbits <= 1;  // a zero block is the single bit "0"
+  uint64_t p = e;
+  uint64_t wi = lo >> 6;     // bitmap word being assembled
+  uint64_t acc = 0;          // this chain's starts in word wi
+  bool merged = false;
+  while (p < hi) {
+    const uint64_t pw = p >> 6;
+    while (wi < pw) {
+      a.bm[wi] = acc;
+      acc = 0;
+      wi++;
+    }
+    const uint32_t sh = (uint32_t)(p & 63);
+    const uint64_t old = check ? a.bm[wi] : 0ull;  // consumed after the parse below
+    const uint64_t h = rd.peek(p);
+    if (runs && !(h & 1)) {
+      // a run of zero blocks, one bit each, within this bitmap word
+      uint32_t c = ctz64(h);
+      const uint32_t room = 64 - sh;
+      c = c < room ? c : room;
+      if ((uint64_t)c > hi - p)
+        c = (uint32_t)(hi - p);
+      const uint64_t m = (c >= 64 ? ~0ull : ((1ull << c) - 1)) << sh;
+      const uint64_t hit = old & m;
+      if (hit) {
+        const uint64_t below = (1ull << ctz64(hit)) - 1;  // this chain's starts before the merge
+        a.bm[wi] = acc | (m & below) | (old & ~below);
+        merged = true;
+        break;
+      }
+      acc |= m;
+      p += c;
+      continue;
+    }
+    const uint32_t len = scan_block<S, DIMS, REV>(rd, p, a.sp);
+    if ((old >> sh) & 1) {
+      // the chain of this segment already has a block at p: from here on the
+      // two chains are the same
+      a.bm[wi] = acc | (old & ~((1ull << sh) - 1));
+      merged = true;
+      break;
+    }
+    acc |= 1ull << sh;
+    p += len;
+  }
+  if (merged)
+    return;
+  a.bm[wi] = acc;
+  const uint64_t wend = (hi + 63) >> 6;
+  for (uint64_t j = wi + 1; j < wend; j++)
+    a.bm[j] = 0;
+  if (!a.first && a.x[s] != p)
+    atomicAdd(a.moved, 1u);
+  a.x[s] = p;
+}
+
+template <typename S, int DIMS, bool REV>
+__global__ __launch_bounds__(256) void scan_pass(ScanArgs a)
+{
+  __shared__ uint64_t rings[256 * (kRing + 1)];  // odd stride: fewer bank collisions
+  const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (s >= a.nseg)
+    return;
+  scan_segment<S, DIMS, REV>(a, s, rings + threadIdx.x * (kRing + 1));
+}
+
+// ---------------------------------------------------------------------------
+// bitmap -> block index.  Tiles of kTileWords bitmap words per 256-thread group.
+constexpr uint32_t kTileWords = 2048;
+
+__global__ __launch_bounds__(256) void bm_tile_count(const uint64_t* __restrict__ bm, uint64_t nwords,
+                                                     uint64_t* __restrict__ tile_cnt)
+{
+  __shared__ uint32_t red[256];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTileWords;
+  uint32_t c = 0;
+  for (uint32_t j = threadIdx.x; j < kTileWords; j += 256) {
+    const uint64_t i = t0 + j;
+    if (i < nwords)
+      c += (uint32_t)__popcll(bm[i]);
+  }
+  red[threadIdx.x] = c;
+  __syncthreads();
+  for (uint32_t d = 128; d > 0; d >>= 1) {
+    if (threadIdx.x < d)
+      red[threadIdx.x] += red[threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    tile_cnt[blockIdx.x] = red[0];
+}
+
+// exclusive scan of n tile counts in place (one 1024-thread group); total -> *sum
+__global__ __launch_bounds__(1024) void tile_scan(uint64_t* __restrict__ v, uint64_t n, uint64_t* __restrict__ sum)
+{
+  __shared__ uint64_t part[1024];
+  const uint64_t per = (n + 1023) / 1024;
+  const uint64_t b = threadIdx.x * per;
+  uint64_t s = 0;
+  for (uint64_t i = b; i < b + per && i < n; i++)
+    s += v[i];
+  part[threadIdx.x] = s;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    uint64_t y = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint64_t run = part[threadIdx.x] - s;
+  for (uint64_t i = b; i < b + per && i < n; i++) {
+    const uint64_t c = v[i];
+    v[i] = run;
+    run += c;
+  }
+  if (threadIdx.x == 1023)
+    *sum = part[1023];
+}
+
+// Set bit r of the bitmap with rank k (0-based) gives pos[k] = r, for k <= nb.
+__global__ __launch_bounds__(256) void bm_tile_emit(const uint64_t* __restrict__ bm, uint64_t nwords,
+                                                    const uint64_t* __restrict__ tile_off, uint64_t nb,
+                                                    uint64_t* __restrict__ pos)
+{
+  __shared__ uint32_t part[256];
+  constexpr uint32_t kPer = kTileWords / 256;  // consecutive words per thread
+  const uint64_t t0 = (uint64_t)blockIdx.x * kTileWords + (uint64_t)threadIdx.x * kPer;
+  uint64_t w[kPer];
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; j++) {
+    w[j] = t0 + j < nwords ? bm[t0 + j] : 0ull;
+    c += (uint32_t)__popcll(w[j]);
+  }
+  part[threadIdx.x] = c;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {
+    uint32_t y = threadIdx.x >= d ? part[threadIdx.x - d] : 0;
+    __syncthreads();
+    part[threadIdx.x] += y;
+    __syncthreads();
+  }
+  uint64_t k = tile_off[blockIdx.x] + part[threadIdx.x] - c;
+  if (k > nb)
+    return;
+#pragma unroll
+  for (uint32_t j = 0; j < kPer; j++) {
+    uint64_t x = w[j];
+    while (x) {
+      if (k > nb)
+        return;
+      const uint32_t b = (uint32_t)__builtin_ctzll(x);
+      pos[k++] = (t0 + j) * 64 + b;
+      x &= x - 1;
+    }
+  }
+}
+
+// decoder index: per-block lengths and per-wave (nbw blocks) start offsets
+__global__ __launch_bounds__(256) void index_from_pos(const uint64_t* __restrict__ pos, uint64_t nb, uint32_t nbw,
+                                                      uint16_t* __restrict__ len, uint64_t* __restrict__ base)
+{
+  const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (b >= nb)
+    return;
+  len[b] = (uint16_t)(pos[b + 1] - pos[b]);
+  if (b % nbw == 0)
+    base[b / nbw] = pos[b];
+}
+
+}  // namespace zfp_amd

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "kernels4.h"
+#include "scan.h"
 #include "zfp_hip.h"
 
 using namespace zfp_amd;
@@ -54,14 +55,52 @@ struct zfp_hip_index {
   int device = -1;
   uint64_t nblocks = 0;
   uint64_t nwaves = 0;
+  uint32_t per_wave = 0;       // blocks per wave of the layout it was made for (64: 3D, 16: 4D)
+  uint64_t start_bit = ~0ull;  // stream bit offset of block 0 it was made for
   uint64_t total_bits = 0;
   uint16_t* d_len = nullptr;   // per-block bit length
   uint64_t* d_base = nullptr;  // per-wave start bit relative to the stream's first block
   size_t cap_blocks = 0, cap_waves = 0;
 };
 
+static int index_reserve(zfp_hip_index* x, uint64_t nblocks, uint64_t nwaves)
+{
+  if (x->cap_blocks < nblocks) {
+    if (x->d_len) (void)hipFree(x->d_len);
+    x->d_len = nullptr;
+    x->cap_blocks = 0;
+    if (hipMalloc(&x->d_len, std::max<uint64_t>(nblocks, 1) * sizeof(uint16_t)) != hipSuccess)
+      return fail("hipMalloc of the block index (%llu blocks) failed", (unsigned long long)nblocks);
+    x->cap_blocks = nblocks;
+  }
+  if (x->cap_waves < nwaves) {
+    if (x->d_base) (void)hipFree(x->d_base);
+    x->d_base = nullptr;
+    x->cap_waves = 0;
+    if (hipMalloc(&x->d_base, std::max<uint64_t>(nwaves, 1) * sizeof(uint64_t)) != hipSuccess)
+      return fail("hipMalloc of the block index (%llu waves) failed", (unsigned long long)nwaves);
+    x->cap_waves = nwaves;
+  }
+  return 1;
+}
+
+static void index_release(zfp_hip_index* x)
+{
+  if (x->d_len) (void)hipFree(x->d_len);
+  if (x->d_base) (void)hipFree(x->d_base);
+  x->d_len = nullptr;
+  x->d_base = nullptr;
+  x->cap_blocks = x->cap_waves = 0;
+  x->nblocks = x->nwaves = 0;
+  x->start_bit = ~0ull;
+}
+
 // ---------------------------------------------------------------------------
-// per-thread, per-device context
+// device contexts: a HIP stream, events and reusable scratch.  Calls borrow a
+// context from a process-wide pool and return it when they finish, so the
+// number of contexts (and their device memory) is bounded by the peak number
+// of concurrent calls, whatever threads make them (zfpy builds a new thread
+// pool per call).  zfp_hip_release_scratch() frees the idle ones.
 struct Scratch {
   void* p = nullptr;
   size_t bytes = 0;
@@ -70,45 +109,77 @@ struct Scratch {
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
-  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // [4], [5]: index scan
   Scratch field, words, status, partials, misc;
-  double kernel_ms = 0, total_ms = 0;
-  bool timed = false;
+  Scratch scan_bm, scan_seg, scan_tiles, scan_pos;  // index scan of a stream without index
+  zfp_hip_index scan_index;                         // index built by the scan
 };
 
-static thread_local std::vector<Ctx*> t_ctx;
-static thread_local Ctx* t_last = nullptr;
+struct Timing {
+  double kernel_ms = 0, total_ms = 0, scan_ms = 0;
+  int scan_passes = 0;
+  bool timed = false;
+};
+static thread_local Timing t_timing;
+
+static std::mutex g_pool_mu;
+static std::vector<Ctx*> g_idle;
+
+static void free_scratch(Scratch& s)
+{
+  if (s.p)
+    (void)hipFree(s.p);
+  s.p = nullptr;
+  s.bytes = 0;
+}
+
+static void destroy_ctx(Ctx* c)
+{
+  (void)hipSetDevice(c->device);
+  for (Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->scan_bm, &c->scan_seg,
+                     &c->scan_tiles, &c->scan_pos})
+    free_scratch(*s);
+  index_release(&c->scan_index);
+  for (auto& e : c->ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream)
+    (void)hipStreamDestroy(c->stream);
+  delete c;
+}
 
 static int ensure(Scratch& s, size_t bytes)
 {
   if (s.bytes >= bytes)
     return 1;
-  if (s.p)
-    (void)hipFree(s.p);
-  s.p = nullptr;
-  s.bytes = 0;
+  free_scratch(s);
   size_t want = std::max(bytes, (size_t)4096);
   hipError_t e = hipMalloc(&s.p, want);
-  if (e != hipSuccess)
+  if (e != hipSuccess) {
+    s.p = nullptr;
     return fail("hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+  }
   s.bytes = want;
   return 1;
 }
 
-static Ctx* get_ctx(int device)
+static Ctx* acquire_ctx(int device)
 {
   if (device < 0) {
     if (hipGetDevice(&device) != hipSuccess)
       device = 0;
   }
-  for (Ctx* c : t_ctx)
-    if (c->device == device) {
-      (void)hipSetDevice(device);
-      return c;
-    }
   if (hipSetDevice(device) != hipSuccess) {
     fail("hipSetDevice(%d) failed", device);
     return nullptr;
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (size_t i = 0; i < g_idle.size(); i++)
+      if (g_idle[i]->device == device) {
+        Ctx* c = g_idle[i];
+        g_idle.erase(g_idle.begin() + (long)i);
+        return c;
+      }
   }
   Ctx* c = new Ctx;
   c->device = device;
@@ -119,9 +190,25 @@ static Ctx* get_ctx(int device)
   }
   for (auto& e : c->ev)
     (void)hipEventCreate(&e);
-  t_ctx.push_back(c);
   return c;
 }
+
+static void release_ctx(Ctx* c)
+{
+  if (!c)
+    return;
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  g_idle.push_back(c);
+}
+
+// borrows a context for the lifetime of one API call
+struct CtxLease {
+  Ctx* c;
+  explicit CtxLease(int device) : c(acquire_ctx(device)) {}
+  ~CtxLease() { release_ctx(c); }
+  CtxLease(const CtxLease&) = delete;
+  CtxLease& operator=(const CtxLease&) = delete;
+};
 
 static bool is_device_ptr(const void* p)
 {
@@ -281,21 +368,13 @@ static int general_args(Ctx* c, const Plan& p, uint64_t nwaves, uint32_t swp, ui
   a.error = (uint32_t*)((char*)c->misc.p + 12);
   a.partials = (Partial*)c->partials.p;
   if (var && index) {
-    if (index->cap_blocks < p.g.nblocks) {
-      if (index->d_len) (void)hipFree(index->d_len);
-      index->d_len = nullptr;
-      HIP_TRY(hipMalloc(&index->d_len, p.g.nblocks * sizeof(uint16_t)));
-      index->cap_blocks = p.g.nblocks;
-    }
-    if (index->cap_waves < nwaves) {
-      if (index->d_base) (void)hipFree(index->d_base);
-      index->d_base = nullptr;
-      HIP_TRY(hipMalloc(&index->d_base, nwaves * sizeof(uint64_t)));
-      index->cap_waves = nwaves;
-    }
+    if (!index_reserve(index, p.g.nblocks, nwaves))
+      return 0;
     index->device = c->device;
     index->nblocks = p.g.nblocks;
     index->nwaves = nwaves;
+    index->per_wave = p.dims == 4 ? kBlocks4PerWave : 64u;
+    index->start_bit = ~0ull;  // set by the caller once the encode succeeded
     a.idx_len = index->d_len;
     a.idx_base = index->d_base;
   }
@@ -524,11 +603,10 @@ static void record_timing(Ctx* c)
   float k = 0, t = 0;
   if (hipEventElapsedTime(&k, c->ev[1], c->ev[2]) == hipSuccess &&
       hipEventElapsedTime(&t, c->ev[0], c->ev[3]) == hipSuccess) {
-    c->kernel_ms = k;
-    c->total_ms = t;
-    c->timed = true;
+    t_timing.kernel_ms = k;
+    t_timing.total_ms = t;
+    t_timing.timed = true;
   }
-  t_last = c;
 }
 
 // copy the box of elements between a host field and a device image of its
@@ -579,6 +657,146 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
 }
 
 // ---------------------------------------------------------------------------
+// Index scan (scan.h): block starts of a variable-rate stream resident on the
+// device at d_in (word 0 holds bit g0 of the first block), written into `x`.
+static uint64_t scan_seg_bits(uint64_t limit)
+{
+  if (const char* e = getenv("ZFP_HIP_SCAN_SEG_BITS")) {
+    const uint64_t v = strtoull(e, nullptr, 10);
+    if (v >= 64)
+      return v & ~63ull;
+  }
+  // about 2^18 lanes at most; segments of at least 16 Kbit so that small
+  // streams need few passes
+  uint64_t L = (limit + (1ull << 18) - 1) >> 18;
+  L = std::max<uint64_t>(L, 16384);
+  return (L + 63) & ~63ull;
+}
+
+template <typename S, int DIMS, bool REV>
+static void launch_scan_pass(Ctx* c, const ScanArgs& a)
+{
+  const unsigned grid = (unsigned)((a.nseg + 255) / 256);
+  hipLaunchKernelGGL((scan_pass<S, DIMS, REV>), dim3(grid), dim3(256), 0, c->stream, a);
+}
+
+static void launch_scan_dispatch(Ctx* c, const Plan& p, const ScanArgs& a)
+{
+  const bool rev = p.cp.minexp < kMinExp;
+  if (p.dbl) {
+    if (p.dims == 4) {
+      if (rev) launch_scan_pass<double, 4, true>(c, a);
+      else launch_scan_pass<double, 4, false>(c, a);
+    } else {
+      if (rev) launch_scan_pass<double, 3, true>(c, a);
+      else launch_scan_pass<double, 3, false>(c, a);
+    }
+  } else {
+    if (p.dims == 4) {
+      if (rev) launch_scan_pass<float, 4, true>(c, a);
+      else launch_scan_pass<float, 4, false>(c, a);
+    } else {
+      if (rev) launch_scan_pass<float, 3, true>(c, a);
+      else launch_scan_pass<float, 3, false>(c, a);
+    }
+  }
+}
+
+static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
+                      zfp_hip_index* x)
+{
+  const uint64_t nb = p.g.nblocks;
+  const uint32_t per_wave = p.dims == 4 ? kBlocks4PerWave : 64u;
+  const uint64_t nwaves = (nb + per_wave - 1) / per_wave;
+  const uint64_t avail = in_words * 64 > g0 ? in_words * 64 - g0 : 0;
+  const uint64_t extent = std::min<uint64_t>(avail, nb * (uint64_t)p.max_len);
+  const uint64_t limit = extent + 1;  // bit positions 0..extent may start a block (or end the last)
+  const uint64_t seg = scan_seg_bits(limit);
+  const uint64_t nseg = (limit + seg - 1) / seg;
+  const uint64_t bm_words = (limit + 63) / 64;
+  const uint64_t ntiles = (bm_words + kTileWords - 1) / kTileWords;
+  if (!ensure(c->scan_bm, bm_words * 8) || !ensure(c->scan_seg, nseg * 3 * 8 + 64) ||
+      !ensure(c->scan_tiles, ntiles * 8 + 64) || !ensure(c->scan_pos, (nb + 1) * 8) ||
+      !index_reserve(x, nb, nwaves))
+    return 0;
+  hipEvent_t e0 = c->ev[4], e1 = c->ev[5];
+  HIP_TRY(hipEventRecord(e0, c->stream));
+  uint64_t* bm = (uint64_t*)c->scan_bm.p;
+  uint64_t* used = (uint64_t*)c->scan_seg.p;
+  uint64_t* xs = used + nseg;
+  uint64_t* xsnap = xs + nseg;
+  uint32_t* moved = (uint32_t*)(xsnap + nseg);
+  HIP_TRY(hipMemsetAsync(bm, 0, bm_words * 8, c->stream));
+  HIP_TRY(hipMemsetAsync(used, 0xff, nseg * 8, c->stream));
+  ScanArgs a{};
+  a.in = d_in;
+  a.in_words = in_words;
+  a.g0 = g0;
+  a.first = 1;
+  a.seg_bits = seg;
+  a.nseg = nseg;
+  a.limit = limit;
+  a.bm = bm;
+  a.entry_used = used;
+  a.xsnap = xsnap;
+  a.x = xs;
+  a.moved = moved;
+  a.sp = ScanParams{p.cp.minbits, p.cp.maxbits, p.cp.maxprec, p.cp.minexp};
+  launch_scan_dispatch(c, p, a);
+  HIP_TRY(hipGetLastError());
+  a.first = 0;
+  int passes = 1;
+  for (;;) {
+    uint32_t host_moved = 0;
+    HIP_TRY(hipMemcpyAsync(xsnap, xs, nseg * 8, hipMemcpyDeviceToDevice, c->stream));
+    HIP_TRY(hipMemsetAsync(moved, 0, 4, c->stream));
+    launch_scan_dispatch(c, p, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(&host_moved, moved, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    passes++;
+    if (!host_moved)
+      break;
+    if ((uint64_t)passes > nseg + 2)
+      return fail("zfp_hip: index scan did not converge after %d passes", passes);
+  }
+  // bitmap -> positions -> index
+  uint64_t* tiles = (uint64_t*)c->scan_tiles.p;
+  uint64_t* sum = tiles + ntiles;
+  uint64_t* pos = (uint64_t*)c->scan_pos.p;
+  hipLaunchKernelGGL(bm_tile_count, dim3((unsigned)ntiles), dim3(256), 0, c->stream, bm, bm_words, tiles);
+  hipLaunchKernelGGL(tile_scan, dim3(1), dim3(1024), 0, c->stream, tiles, ntiles, sum);
+  hipLaunchKernelGGL(bm_tile_emit, dim3((unsigned)ntiles), dim3(256), 0, c->stream, bm, bm_words, tiles, nb, pos);
+  hipLaunchKernelGGL(index_from_pos, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, c->stream, pos, nb, per_wave,
+                     x->d_len, x->d_base);
+  HIP_TRY(hipGetLastError());
+  uint64_t host[2] = {0, 0};
+  HIP_TRY(hipMemcpyAsync(&host[0], sum, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(&host[1], pos + nb, 8, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipEventRecord(e1, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (host[0] < nb + 1)
+    return fail("zfp_hip: stream holds %llu of %llu blocks (truncated or not a stream of this field/mode)",
+                (unsigned long long)(host[0] ? host[0] - 1 : 0), (unsigned long long)nb);
+  float ms = 0;
+  if (hipEventElapsedTime(&ms, e0, e1) == hipSuccess)
+    t_timing.scan_ms = ms;
+  t_timing.scan_passes = passes;
+  x->device = c->device;
+  x->nblocks = nb;
+  x->nwaves = nwaves;
+  x->per_wave = per_wave;
+  x->total_bits = host[1];
+  return 1;
+}
+
+static bool index_matches(const zfp_hip_index* x, const Plan& p, uint64_t bit_offset, int device)
+{
+  return x && x->d_len && x->nblocks == p.g.nblocks && x->start_bit == bit_offset && x->device == device &&
+         x->per_wave == (p.dims == 4 ? kBlocks4PerWave : 64u);
+}
+
+// ---------------------------------------------------------------------------
 extern "C" {
 
 int zfp_hip_device_count(void)
@@ -603,9 +821,11 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
     return fail("zfp_hip_compress: null field or stream pointer");
   if (zfp_hip_device_count() <= 0)
     return fail("zfp_hip_compress: no HIP device available");
-  Ctx* c = get_ctx(device);
+  CtxLease lease(device);
+  Ctx* c = lease.c;
   if (!c)
     return 0;
+  t_timing = Timing{};
   const size_t es = p.dbl ? 8 : 4;
   const uint64_t W0 = bit_offset >> 6;
   const uint32_t g0 = (uint32_t)(bit_offset & 63);
@@ -659,6 +879,8 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   record_timing(c);
+  if (index && !p.fixed)
+    index->start_bit = bit_offset;
   *end_bit = end;
   return 1;
 }
@@ -673,15 +895,11 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
     return fail("zfp_hip_decompress: null field or stream pointer");
   if (zfp_hip_device_count() <= 0)
     return fail("zfp_hip_decompress: no HIP device available");
-  if (!p.fixed) {
-    if (!index || !index->d_len || index->nblocks != p.g.nblocks)
-      return fail("zfp_hip_decompress: variable-rate stream needs the block index produced by its compression");
-  }
-  Ctx* c = get_ctx(device);
+  CtxLease lease(device);
+  Ctx* c = lease.c;
   if (!c)
     return 0;
-  if (!p.fixed && index->device != c->device)
-    return fail("zfp_hip_decompress: block index lives on device %d, decoding on %d", index->device, c->device);
+  t_timing = Timing{};
   const size_t es = p.dbl ? 8 : 4;
   const uint64_t W0 = bit_offset >> 6;
   const uint32_t g0 = (uint32_t)(bit_offset & 63);
@@ -689,8 +907,19 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
     *end_bit = bit_offset;
     return 1;
   }
-  const uint64_t total = p.fixed ? p.g.nblocks * (uint64_t)p.cp.maxbits : index->total_bits;
-  const uint64_t nwords = std::min<uint64_t>((g0 + total + 63) / 64 + 1, capacity_words > W0 ? capacity_words - W0 : 0);
+  // a variable-rate stream without a matching index (made by another
+  // process, another library, or for another position) is scanned
+  const bool have_index = !p.fixed && index_matches(index, p, bit_offset, c->device);
+  const bool scan = !p.fixed && !have_index;
+  const uint64_t avail = capacity_words > W0 ? capacity_words - W0 : 0;
+  uint64_t nwords;
+  if (p.fixed)
+    nwords = (g0 + p.g.nblocks * (uint64_t)p.cp.maxbits + 63) / 64 + 1;
+  else if (have_index)
+    nwords = (g0 + index->total_bits + 63) / 64 + 1;
+  else
+    nwords = (g0 + p.g.nblocks * (uint64_t)p.max_len + 63) / 64 + 1;
+  nwords = std::min<uint64_t>(nwords, avail);
   const bool dev_field = is_device_ptr(field_base);
   const bool dev_stream = is_device_ptr(words);
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
@@ -701,6 +930,13 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
     HIP_TRY(hipMemcpyAsync(c->words.p, words + W0, nwords * 8, hipMemcpyHostToDevice, c->stream));
     d_in = (const uint64_t*)c->words.p;
   }
+  if (scan) {
+    if (!scan_index(c, p, d_in, nwords, g0, &c->scan_index))
+      return 0;
+    c->scan_index.start_bit = bit_offset;
+    index = &c->scan_index;
+  }
+  const uint64_t total = p.fixed ? p.g.nblocks * (uint64_t)p.cp.maxbits : index->total_bits;
   void* d_field = field_base;
   char* d_img = nullptr;
   if (!dev_field) {
@@ -723,14 +959,54 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
   return 1;
 }
 
+int zfp_hip_index_build(const zfp_hip_job* job, const uint64_t* words, uint64_t capacity_words, uint64_t bit_offset,
+                        int device, zfp_hip_index* index)
+{
+  Plan p;
+  if (!index)
+    return fail("zfp_hip_index_build: null index");
+  if (!plan_job(job, nullptr, p))
+    return 0;
+  if (p.fixed)
+    return fail("zfp_hip_index_build: fixed-rate streams need no index");
+  if (!words)
+    return fail("zfp_hip_index_build: null stream");
+  if (zfp_hip_device_count() <= 0)
+    return fail("zfp_hip_index_build: no HIP device available");
+  CtxLease lease(device);
+  Ctx* c = lease.c;
+  if (!c)
+    return 0;
+  t_timing = Timing{};
+  const uint64_t W0 = bit_offset >> 6;
+  const uint32_t g0 = (uint32_t)(bit_offset & 63);
+  const uint64_t avail = capacity_words > W0 ? capacity_words - W0 : 0;
+  const uint64_t nwords = std::min<uint64_t>((g0 + p.g.nblocks * (uint64_t)p.max_len + 63) / 64 + 1, avail);
+  const uint64_t* d_in = words + W0;
+  if (!is_device_ptr(words)) {
+    if (!ensure(c->words, nwords * 8 + 8))
+      return 0;
+    HIP_TRY(hipMemcpyAsync(c->words.p, words + W0, nwords * 8, hipMemcpyHostToDevice, c->stream));
+    d_in = (const uint64_t*)c->words.p;
+  }
+  if (p.g.nblocks == 0) {
+    index->nblocks = 0;
+    index->nwaves = 0;
+    index->total_bits = 0;
+  } else if (!scan_index(c, p, d_in, nwords, g0, index)) {
+    return 0;
+  }
+  index->start_bit = bit_offset;
+  return 1;
+}
+
 zfp_hip_index* zfp_hip_index_create(void) { return new zfp_hip_index; }
 
 void zfp_hip_index_free(zfp_hip_index* index)
 {
   if (!index)
     return;
-  if (index->d_len) (void)hipFree(index->d_len);
-  if (index->d_base) (void)hipFree(index->d_base);
+  index_release(index);
   delete index;
 }
 
@@ -740,17 +1016,19 @@ size_t zfp_hip_index_export(const zfp_hip_index* index, void* buffer, size_t cap
 {
   if (!index)
     return 0;
-  size_t need = 32 + index->nblocks * 2 + index->nwaves * 8;
+  size_t need = 48 + index->nblocks * 2 + index->nwaves * 8;
   if (!buffer)
     return need;
   if (capacity < need)
     return 0;
   uint64_t* h = (uint64_t*)buffer;
-  h[0] = 0x7a6678646e69ull;  // tag
+  h[0] = 0x327a6678646e69ull;  // tag ("indxfz2")
   h[1] = index->nblocks;
   h[2] = index->nwaves;
   h[3] = index->total_bits;
-  char* q = (char*)buffer + 32;
+  h[4] = index->per_wave;
+  h[5] = index->start_bit;
+  char* q = (char*)buffer + 48;
   if (index->nblocks && hipMemcpy(q, index->d_len, index->nblocks * 2, hipMemcpyDeviceToHost) != hipSuccess)
     return 0;
   q += index->nblocks * 2;
@@ -761,17 +1039,19 @@ size_t zfp_hip_index_export(const zfp_hip_index* index, void* buffer, size_t cap
 
 zfp_hip_index* zfp_hip_index_import(const void* buffer, size_t bytes)
 {
-  if (!buffer || bytes < 32)
+  if (!buffer || bytes < 48)
     return nullptr;
   const uint64_t* h = (const uint64_t*)buffer;
-  if (h[0] != 0x7a6678646e69ull || bytes < 32 + h[1] * 2 + h[2] * 8)
+  if (h[0] != 0x327a6678646e69ull || bytes < 48 + h[1] * 2 + h[2] * 8)
     return nullptr;
   zfp_hip_index* x = new zfp_hip_index;
   x->nblocks = h[1];
   x->nwaves = h[2];
   x->total_bits = h[3];
+  x->per_wave = (uint32_t)h[4];
+  x->start_bit = h[5];
   (void)hipGetDevice(&x->device);
-  const char* q = (const char*)buffer + 32;
+  const char* q = (const char*)buffer + 48;
   if ((x->nblocks && hipMalloc(&x->d_len, x->nblocks * 2) != hipSuccess) ||
       (x->nwaves && hipMalloc(&x->d_base, x->nwaves * 8) != hipSuccess)) {
     zfp_hip_index_free(x);
@@ -788,11 +1068,45 @@ zfp_hip_index* zfp_hip_index_import(const void* buffer, size_t bytes)
 
 int zfp_hip_last_timing(double* kernel_ms, double* total_ms)
 {
-  if (!t_last || !t_last->timed)
+  if (!t_timing.timed)
     return 0;
-  if (kernel_ms) *kernel_ms = t_last->kernel_ms;
-  if (total_ms) *total_ms = t_last->total_ms;
+  if (kernel_ms) *kernel_ms = t_timing.kernel_ms;
+  if (total_ms) *total_ms = t_timing.total_ms;
   return 1;
+}
+
+int zfp_hip_last_scan(double* scan_ms, int* passes)
+{
+  if (!t_timing.scan_passes)
+    return 0;
+  if (scan_ms) *scan_ms = t_timing.scan_ms;
+  if (passes) *passes = t_timing.scan_passes;
+  return 1;
+}
+
+size_t zfp_hip_scratch_bytes(void)
+{
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  size_t b = 0;
+  for (Ctx* c : g_idle) {
+    for (const Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->scan_bm, &c->scan_seg,
+                             &c->scan_tiles, &c->scan_pos})
+      b += s->bytes;
+    b += c->scan_index.cap_blocks * 2 + c->scan_index.cap_waves * 8;
+  }
+  return b;
+}
+
+int zfp_hip_release_scratch(void)
+{
+  std::vector<Ctx*> idle;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    idle.swap(g_idle);
+  }
+  for (Ctx* c : idle)
+    destroy_ctx(c);
+  return (int)idle.size();
 }
 
 }  // extern "C"

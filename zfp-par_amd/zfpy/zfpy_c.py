@@ -11,7 +11,11 @@ Additions (keyword-only, optional):
   * arrays exposing __cuda_array_interface__ (e.g. torch CUDA tensors) are
     accepted by compress_numpy and compressed straight from device memory;
   * variable-rate streams carry their GPU block index as an attribute of the
-    returned bytes object (`ZfpBytes.block_index`); decompress uses it.
+    returned bytes object (`ZfpBytes.block_index`), an optional shortcut:
+    decompress uses it when present and otherwise (plain bytes, a file, a
+    stream from another library) finds the block starts on the GPU by a
+    parallel parse of the stream (zfp_hip_index_build), so any valid stream
+    decodes, as with the reference.
 """
 import ctypes
 import itertools

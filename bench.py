@@ -1,30 +1,43 @@
 #!/usr/bin/env python3
 """Benchmark: GB/s uncompressed, 3D float32 fixed-rate encode, device-resident.
 
-One step = zfp_compress of one 1024^3 float32 field at rate 16 (BASELINE.json
-configs[1]) through the drop-in C API, with the field and the stream buffer
-already in HBM.  With N GPUs (one process per GPU, torchrun) each rank
-compresses its own 1024^3 z-slab chunk of an N*1024-plane field: chunks are
-independent zfp streams, so the timed region has no collective (weak scaling);
-the RCCL gather that concatenates the chunk streams on rank 0 is timed
-separately and reported as `gather_*`.
+Workloads (--workload):
+  c2 (default)  one step = zfp_compress of one 1024^3 float32 field at rate 16
+                (BASELINE.json configs[1]) through the drop-in C API, field and
+                stream already in HBM.  With N GPUs each rank compresses its own
+                1024^3 z-slab chunk of an N*1024-plane field (weak scaling).
+  c4            one step = the zfpy chunk stream of configs[3]: per rank one
+                4096x4096x64 float32 z-slab of the 4096x4096x512 field, rate 8,
+                written after the 96-bit whole-field header exactly as
+                compress_numpy_portion lays it out (python/zfpy_c.pyx:330-376).
+Chunks are independent zfp streams, so the timed region has no collective; the
+RCCL gather that concatenates the chunk streams on rank 0 is timed separately
+and reported as `gather`, never inside `value`.
+
+--gpus N without WORLD_SIZE in the environment re-launches this script under
+torch.distributed.run with N ranks (before anything touches a GPU) and exits
+with its status.  --dry-run runs the launcher, barriers and max-over-ranks
+timing on CPU with gloo (a numpy copy stands in for the codec) -- for tests.
 
 Printed JSON (rank 0): the contract keys plus
   roofline      dominant kernel (encode3_aligned) against HBM peak: achieved =
-                algorithmic bytes per launch (4 B read + 2 B written per value)
+                algorithmic bytes per launch (4 B read + R/8 B written per value)
                 / mean kernel time from HIP events on the kernel's own stream;
                 traffic = PMC HBM bytes per launch from profiles/*pmc*.json
                 (rocprofv3 pass, gfx950 FETCH_SIZE x2 correction) or null
   cpu_baseline  the reference itself (oracle/_ref/libzfp_ref.so, compiled from
-                /root/reference), OpenMP, on this host's cores, bounded sample
+                /root/reference), OpenMP, every core this process may use, on
+                the full per-GPU field (c2)
   decode_*      zfp_decompress of the same stream (same field, device-resident)
-  bitexact      GPU stream bytes == reference CPU stream bytes on the sample
+  bitexact      GPU stream bytes == reference CPU stream bytes (whole field)
 """
 import argparse
 import ctypes
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -38,11 +51,35 @@ for p in (REPO, os.path.join(REPO, "tests"), os.path.join(REPO, "oracle")):
 METRIC = "GB/s uncompressed, 3D float32 fixed-rate encode, device-resident"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 N = 1024
-RATE = 16
 
 
-def smooth_field_torch(torch, nx, ny, nz, z0, ntot_z, device):
-    """F1: v = sin(.05x) cos(.03y) + .5 sin(.02z + .01 x y / n), x fastest."""
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", choices=("c2", "c4"), default="c2")
+    ap.add_argument("--n", type=int, default=N, help="c2: edge of the per-GPU cube (default 1024)")
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--dry-run", action="store_true", help="CPU/gloo plumbing check, no GPU")
+    return ap.parse_args(argv)
+
+
+def relaunch(args):
+    """Start N ranks under torch.distributed.run as a child process (this
+    process has not initialised HIP) and return its exit status."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def smooth_slab_torch(torch, nx, ny, nz, z0, device):
+    """F1: v = sin(.05x) cos(.03y) + .5 sin(.02z + .01 x y / nx), x fastest, planes z0.."""
     x = torch.arange(nx, device=device, dtype=torch.float64)
     y = torch.arange(ny, device=device, dtype=torch.float64)
     out = torch.empty((nz, ny, nx), device=device, dtype=torch.float32)
@@ -56,25 +93,45 @@ def smooth_field_torch(torch, nx, ny, nz, z0, ntot_z, device):
 
 def load_capi(path):
     from capi import ZfpCAPI
-    api = ZfpCAPI(path)
-    return api
+    return ZfpCAPI(path)
 
 
-def traffic_from_profiles():
-    """Per-launch HBM bytes of encode3_aligned from a committed PMC summary, if any."""
+def traffic_from_profiles(kernel="encode3_aligned"):
+    """Per-launch HBM bytes of the dominant kernel from a committed PMC summary, if any."""
     files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            if "encode3_aligned" in d and d["encode3_aligned"].get("hbm_bytes_per_launch"):
-                return d["encode3_aligned"]["hbm_bytes_per_launch"], os.path.basename(f)
+            if kernel in d and d[kernel].get("hbm_bytes_per_launch"):
+                return d[kernel]["hbm_bytes_per_launch"], os.path.basename(f)
         except Exception:
             continue
     return None, None
 
 
-def cpu_baseline(field_np, threads):
-    """The reference library (OpenMP policy) on a bounded slab; returns (GB/s, bytes)."""
+def host_cores():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) / int(per)))
+    except Exception:
+        pass
+    model = None
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except Exception:
+        pass
+    return min(aff, quota) if quota else aff, aff, quota, model
+
+
+def cpu_baseline(field_np, rate, threads):
+    """The reference library (OpenMP policy) on the whole field; returns (GB/s, stream bytes, best s)."""
     from pyoracle import REF_SO
     if not os.path.exists(REF_SO):
         return None
@@ -83,7 +140,7 @@ def cpu_baseline(field_np, threads):
     ref.lib.zfp_stream_set_omp_threads.argtypes = [ctypes.c_void_p, ctypes.c_uint]
     f = ref.field_for(field_np)
     zs = ref.lib.zfp_stream_open(None)
-    ref.lib.zfp_stream_set_rate(zs, float(RATE), 3, 3, 0)
+    ref.lib.zfp_stream_set_rate(zs, float(rate), 3, 3, 0)
     ref.lib.zfp_stream_set_omp_threads(zs, threads)
     cap = ref.lib.zfp_stream_maximum_size(zs, f)
     buf = np.zeros(cap, dtype=np.uint8)
@@ -100,17 +157,13 @@ def cpu_baseline(field_np, threads):
     ref.lib.stream_close(bs)
     ref.lib.zfp_stream_close(zs)
     ref.lib.zfp_field_free(f)
-    return field_np.nbytes / best / 1e9, bytes(buf[:nbytes])
+    return field_np.nbytes / best / 1e9, buf[:nbytes], best
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=N, help="edge of the per-GPU cube (default 1024)")
-    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
-    args = ap.parse_args()
+    args = parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch(args))
 
     import torch
     import torch.distributed as dist
@@ -119,35 +172,56 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world > 1
+    if args.dry_run:
+        if distributed:
+            dist.init_process_group("gloo")
+        return dry_run(args, torch, dist, world, rank)
+
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
-    n = args.n
     api = load_capi(os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so"))
     api.enable_index()
     lib = api.lib
     lib.zfp_hip_last_timing.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 
-    # this rank's chunk: z-slab [rank*n, rank*n + n) of an n x n x (world*n) field
-    field_t = smooth_field_torch(torch, n, n, n, rank * n, world * n, dev)
+    if args.workload == "c2":
+        n = args.n
+        nx, ny, nz, rate = n, n, n, 16
+        z0, ztot = rank * n, world * n
+        workload = "%d^3 float32 fixed-rate %d zfp_compress per GPU (BASELINE configs[1])" % (n, rate)
+    else:
+        nx, ny, nz, rate = 4096, 4096, 64, 8
+        z0, ztot = rank * 64, 512
+        workload = ("4096x4096x64 float32 fixed-rate 8 z-slab per GPU = one zfpy chunk of 4096x4096x512 "
+                    "(BASELINE configs[3]), stream after the 96-bit whole-field header")
+    field_t = smooth_slab_torch(torch, nx, ny, nz, z0, dev)
     nvals = field_t.numel()
-    zf = lib.zfp_field_3d(ctypes.c_void_p(field_t.data_ptr()), 3, n, n, n)
+    zf = lib.zfp_field_3d(ctypes.c_void_p(field_t.data_ptr()), 3, nx, ny, nz)
     zs = lib.zfp_stream_open(None)
-    lib.zfp_stream_set_rate(zs, float(RATE), 3, 3, 0)
-    cap = lib.zfp_stream_maximum_size(zs, zf)
+    # zfpy passes zfp_type_none to set_rate (pyx:300-302); the C API bench passes float
+    lib.zfp_stream_set_rate(zs, float(rate), 3 if args.workload == "c2" else 0, 3, 0)
+    cap = lib.zfp_stream_maximum_size(zs, zf) + 64
     out_t = torch.zeros(cap, dtype=torch.uint8, device=dev)
     bs = lib.stream_open(ctypes.c_void_p(out_t.data_ptr()), cap)
     lib.zfp_stream_set_bit_stream(zs, bs)
+    hdr_field = None
+    if args.workload == "c4":
+        # header of the whole 4096x4096x512 field, written into the device stream
+        hdr_field = lib.zfp_field_3d(None, 3, nx, ny, ztot)
 
     def step():
         lib.zfp_stream_rewind(zs)
+        if hdr_field is not None and lib.zfp_write_header(zs, hdr_field, 7) != 96:
+            raise RuntimeError("zfp_write_header failed")
         nb = lib.zfp_compress(zs, zf)
         if nb == 0:
             raise RuntimeError("zfp_compress failed: %s" % lib.zfp_hip_last_error())
         return nb
 
+    nbytes = 0
     for _ in range(args.warmup):
         nbytes = step()
     if distributed:
@@ -165,7 +239,7 @@ def main():
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    ms = elapsed / args.steps * 1e3
+    ms = elapsed / max(1, args.steps) * 1e3
     if distributed:
         tt = torch.tensor([ms], device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -176,7 +250,9 @@ def main():
     lib.zfp_field_set_pointer(zf, ctypes.c_void_p(back_t.data_ptr()))
     dms = []
     for i in range(max(3, args.steps // 2)):
-        lib.stream_rewind(bs)
+        lib.zfp_stream_rewind(zs)
+        if hdr_field is not None:
+            lib.stream_rseek(bs, 96)
         torch.cuda.synchronize()
         t1 = time.perf_counter()
         if lib.zfp_decompress(zs, zf) == 0:
@@ -185,6 +261,10 @@ def main():
         if i:
             dms.append((time.perf_counter() - t1) * 1e3)
     lib.zfp_field_set_pointer(zf, ctypes.c_void_p(field_t.data_ptr()))
+    roundtrip_ok = None
+    if args.workload == "c2":
+        # fixed rate 16 is lossy: report the max error of the round trip
+        roundtrip_ok = float((back_t - field_t).abs().max().item())
 
     # gather of the chunk streams to rank 0 over RCCL (timed separately)
     gather = None
@@ -204,20 +284,22 @@ def main():
         gt = torch.tensor([gms], device=dev)
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
         total_bytes = sum(int(s.item()) for s in all_sizes)
-        gather = {"ms": float(gt.item()), "bytes": total_bytes, "GBps": total_bytes / (float(gt.item()) * 1e6)}
+        gather = {"ms": round(float(gt.item()), 3), "bytes": total_bytes,
+                  "GBps": round(total_bytes / (float(gt.item()) * 1e6), 2), "collective": "RCCL gather to rank 0"}
+        del recv
 
     if rank == 0:
         kernel_ms = float(np.mean(kms))
-        alg_bytes = nvals * 4 + nvals * RATE // 8
+        alg_bytes = nvals * 4 + nvals * rate // 8
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic, tsrc = traffic_from_profiles()
+        traffic, tsrc = traffic_from_profiles() if args.workload == "c2" else (None, None)
         value = world * nvals * 4 / (ms * 1e-3) / 1e9
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "f32", "data": "synthetic (F1 smooth field generated on device)",
-            "config": {"workload": "%d^3 float32 fixed-rate %d zfp_compress per GPU (BASELINE configs[1])" % (n, RATE),
-                       "field_per_gpu": [n, n, n], "rate": RATE, "stream_bytes_per_gpu": int(nbytes),
+            "config": {"workload": workload, "field_per_gpu": [nx, ny, nz], "rate": rate,
+                       "stream_bytes_per_gpu": int(nbytes),
                        "parallelism": "%d independent z-slab chunks, one per GPU" % world},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -226,21 +308,22 @@ def main():
             "call_ms": round(float(np.mean(tms)), 4),
             "decode_ms": round(float(np.mean(dms)), 4) if dms else None,
             "decode_GBps": round(nvals * 4 / (np.mean(dms) * 1e-3) / 1e9, 2) if dms else None,
+            "decode_max_abs_err": roundtrip_ok,
             "gather": gather,
         }
-        if not args.no_cpu and world == 1:
-            threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-            nz_s = min(n, 256)
-            sample = field_t[:nz_s].cpu().numpy()
-            cb = cpu_baseline(sample, threads)
+        if not args.no_cpu and world == 1 and args.workload == "c2":
+            cores, aff, quota, model = host_cores()
+            sample = field_t.cpu().numpy()
+            cb = cpu_baseline(sample, rate, cores)
             if cb is not None:
-                gbs, ref_bytes = cb
-                gpu_bytes = out_t[: len(ref_bytes)].cpu().numpy().tobytes()
-                result["cpu_baseline"] = {"value": round(gbs, 3), "unit": "GB/s", "cores": threads,
-                                          "kind": "reference",
-                                          "sample": "%dx%dx%d z-slab of the same field, zfp_compress exec=omp, best of 3"
-                                                    % (n, n, nz_s)}
-                result["bitexact_vs_reference"] = gpu_bytes == ref_bytes
+                gbs, ref_bytes, best = cb
+                gpu_bytes = out_t[: len(ref_bytes)].cpu().numpy()
+                result["cpu_baseline"] = {
+                    "value": round(gbs, 3), "unit": "GB/s", "cores": cores, "kind": "reference",
+                    "sample": "the full %dx%dx%d field, reference zfp_compress exec=omp with %d threads, best of 3 "
+                              "(%.3f s)" % (nx, ny, nz, cores, best),
+                    "cpu_model": model, "affinity_cpus": aff, "cgroup_cpu_quota": quota}
+                result["bitexact_vs_reference"] = bool(np.array_equal(gpu_bytes, ref_bytes))
             else:
                 result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
@@ -248,6 +331,39 @@ def main():
     lib.stream_close(bs)
     lib.zfp_stream_close(zs)
     lib.zfp_field_free(zf)
+    if hdr_field is not None:
+        lib.zfp_field_free(hdr_field)
+    if distributed:
+        dist.destroy_process_group()
+
+
+def dry_run(args, torch, dist, world, rank):
+    """Launcher/timing plumbing on CPU: a numpy copy of a small field stands in
+    for the codec step; the JSON says so (`dry_run`)."""
+    distributed = world > 1
+    src = np.random.default_rng(rank).standard_normal(1 << 20).astype(np.float32)
+    dst = np.empty_like(src)
+    for _ in range(args.warmup):
+        np.copyto(dst, src)
+    if distributed:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        np.copyto(dst, src)
+    if distributed:
+        dist.barrier()
+    ms = (time.perf_counter() - t0) / max(1, args.steps) * 1e3
+    if distributed:
+        t = torch.tensor([ms])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        ms = float(t.item())
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": round(world * src.nbytes / (ms * 1e-3) / 1e9, 3), "unit": "GB/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
+                          "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+                          "data": "synthetic", "dry_run": True,
+                          "config": {"workload": "dry run: numpy copy of 4 MiB per rank (no codec, no GPU)"}}),
+              flush=True)
     if distributed:
         dist.destroy_process_group()
 

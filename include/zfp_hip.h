@@ -63,6 +63,12 @@ int zfp_hip_device_count(void);
 /* Human-readable description of the last failure on this thread. */
 const char* zfp_hip_last_error(void);
 
+/* 1 if p points into HIP device memory (0 without a GPU).  The host bitstream
+ * (stream_open) uses it to move the words it touches itself with hipMemcpy. */
+int zfp_hip_is_device_ptr(const void* p);
+/* Synchronous copy between any host/device pointers; 0 on failure. */
+int zfp_hip_memcpy(void* dst, const void* src, size_t bytes);
+
 /*
  * Encode the chunk box of `job` into the stream whose word array begins at
  * `words` (capacity `capacity_words` 64-bit words), starting at bit

@@ -811,6 +811,21 @@ int zfp_hip_device_count(void)
 
 const char* zfp_hip_last_error(void) { return g_err.c_str(); }
 
+int zfp_hip_is_device_ptr(const void* p)
+{
+  static int ndev = -1;  // benign race: every thread computes the same value
+  if (ndev < 0)
+    ndev = zfp_hip_device_count();
+  return ndev > 0 && is_device_ptr(p) ? 1 : 0;
+}
+
+int zfp_hip_memcpy(void* dst, const void* src, size_t bytes)
+{
+  if (hipMemcpy(dst, src, bytes, hipMemcpyDefault) != hipSuccess)
+    return fail("hipMemcpy(%zu) failed", bytes);
+  return 1;
+}
+
 int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* words, uint64_t capacity_words,
                      uint64_t bit_offset, uint64_t head_word, int device, zfp_hip_index* index, uint64_t* end_bit)
 {

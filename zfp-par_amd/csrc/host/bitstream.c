@@ -5,16 +5,44 @@
  * partially filled word is held in `buffer` until it fills or the stream is
  * flushed (zero padding).  Reading mirrors that with `buffer` holding the
  * unread high bits of the last fetched word.
+ *
+ * MI355X addition: a stream may live in HIP device memory (stream_open
+ * detects it).  The codec writes such streams on the device; the few words the
+ * host touches itself (headers, seeks) are moved with hipMemcpy, so
+ * zfp_write_header / zfp_read_header work on device-resident streams too.
  */
 #include <stdlib.h>
 
 #include "zfp/bitstream.h"
+#include "zfp_hip.h"
 #include "zfp_internal.h"
 
 const size_t stream_word_bits = 64;
 
-static uint64 load_word(bitstream* s) { return *s->ptr++; }
-static void store_word(bitstream* s, uint64 w) { *s->ptr++ = w; }
+static uint64 peek_word(const bitstream* s)
+{
+  uint64 w = 0;
+  if (!s->device)
+    return *s->ptr;
+  (void)zfp_hip_memcpy(&w, s->ptr, sizeof w);
+  return w;
+}
+
+static uint64 load_word(bitstream* s)
+{
+  uint64 w = peek_word(s);
+  s->ptr++;
+  return w;
+}
+
+static void store_word(bitstream* s, uint64 w)
+{
+  if (s->device)
+    (void)zfp_hip_memcpy(s->ptr, &w, sizeof w);
+  else
+    *s->ptr = w;
+  s->ptr++;
+}
 
 bitstream* stream_open(void* buffer, size_t bytes)
 {
@@ -22,6 +50,7 @@ bitstream* stream_open(void* buffer, size_t bytes)
   if (s) {
     s->begin = (uint64*)buffer;
     s->end = s->begin + bytes / sizeof(uint64);
+    s->device = zfp_hip_is_device_ptr(buffer);
     stream_rewind(s);
   }
   return s;
@@ -140,7 +169,7 @@ void stream_wseek(bitstream* s, bitstream_offset offset)
   size_t r = (size_t)(offset % 64);
   s->ptr = s->begin + (size_t)(offset / 64);
   if (r) {
-    s->buffer = *s->ptr & (((uint64)1 << r) - 1);
+    s->buffer = peek_word(s) & (((uint64)1 << r) - 1);
     s->bits = r;
   } else {
     s->buffer = 0;

@@ -11,6 +11,7 @@ struct bitstream {
   uint64* ptr;   /* next word to be read/written */
   uint64* begin; /* first word */
   uint64* end;   /* one past last word */
+  int device;    /* the word array is HIP device memory: word I/O goes through hipMemcpy */
 };
 
 #endif

@@ -10,9 +10,10 @@ using namespace zfp_amd;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
-// MODE 0: full; 1: no coder (planes folded into one word); 2: coder on synthetic planes; 3: load+max only
+// MODE 0: full; 1: no coder (planes folded into one word); 2: coder on synthetic planes; 3: load+max only;
+// 4: load + cast + lift (no planes, no coder)
 #ifndef KEXP_WPS
-#define KEXP_WPS 4
+#define KEXP_WPS 3
 #endif
 template <int MODE>
 __global__ __launch_bounds__(256, KEXP_WPS) void enc_var(const float* __restrict__ data, Geometry g, CodecParams cp,
@@ -46,6 +47,15 @@ __global__ __launch_bounds__(256, KEXP_WPS) void enc_var(const float* __restrict
       gather3<float, true>(v, data, g, p);
       if (MODE == 0) {
         encode_block3<float, false, true>(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+      } else if (MODE == 4) {
+        int32_t q[64];
+        uint32_t mp;
+        lossy_emax_cast(q, v, cp, mp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+        xform<3, false, false>(q);
+        uint32_t acc = 0;
+#pragma unroll
+        for (int k = 0; k < 64; k++) acc ^= (uint32_t)q[k] + k;
+        os.head(acc);
       } else if (MODE == 1) {
         int32_t q[64];
         uint32_t mp;
@@ -78,6 +88,60 @@ __global__ __launch_bounds__(256, KEXP_WPS) void enc_var(const float* __restrict
   }
 }
 
+
+// persistent + software-pipelined full encoder (prefetch of the next batch's
+// field into registers once the planes are built)
+#ifndef KEXP_PIPE_WPS
+#define KEXP_PIPE_WPS 3
+#endif
+__global__ __launch_bounds__(256, KEXP_PIPE_WPS) void enc_pipe(const float* __restrict__ data, Geometry g, CodecParams cp,
+                                                    uint64_t* __restrict__ out, uint32_t sw, uint32_t swp, uint32_t magic)
+{
+  __shared__ uint32_t lut[256];
+  extern __shared__ uint64_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint64_t* wslot = lds + (size_t)wv * 64 * swp;
+  lut[threadIdx.x] = dbl_entry(threadIdx.x);
+  __syncthreads();
+  const uint64_t nw = (g.nblocks + 63) / 64;
+  const uint64_t step = (uint64_t)gridDim.x * kWavesPerGroup;
+  uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  if (w >= nw) return;
+  uint64_t* slot = wslot + (size_t)lane * swp;
+  float v[64];
+  gather3<float, true>(v, data, g, block_pos(g, w * 64 + lane, 3));
+  for (;;) {
+    for (uint32_t i = 0; i + 1 < swp; i += 2)
+      *reinterpret_cast<ulonglong2*>(slot + i) = make_ulonglong2(0, 0);
+    slot[swp - 1] = 0;
+    const uint64_t wn = w + step;
+    const uint64_t b = w * 64 + lane;
+    if (b < g.nblocks) {
+      const BlockPos p = block_pos(g, b, 3);
+      OrSlot os{slot, 2 * swp - 1};
+      encode_block3_fixed(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); },
+                          [&] {
+                            if (wn < nw)
+                              gather3<float, true>(v, data, g, block_pos(g, wn * 64 + lane, 3));
+                          });
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = 64 * sw;
+    uint64_t* dst = out + w * 64 * sw;
+    for (uint32_t i = 2 * lane; i < total; i += 128) {
+      const uint32_t l = div_magic(i, magic);
+      const uint64_t* src = wslot + (size_t)l * swp + (i - l * sw);
+      ulonglong2 q; q.x = src[0]; q.y = src[1];
+      *reinterpret_cast<ulonglong2*>(dst + i) = q;
+    }
+    __builtin_amdgcn_wave_barrier();
+    w = wn;
+    if (w >= nw) break;
+  }
+}
+
 template <typename K>
 static float time_it(K launch, int reps)
 {
@@ -95,6 +159,7 @@ static float time_it(K launch, int reps)
 
 int main()
 {
+  setvbuf(stdout, nullptr, _IOLBF, 0);
   const uint64_t n = 1024;
   const size_t N = n * n * n;
   float* d; uint64_t* o;
@@ -127,5 +192,24 @@ int main()
   printf("coder-only  %.3f ms\n", t);
   t = time_it([&] { hipLaunchKernelGGL(enc_var<3>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 10);
   printf("load-only   %.3f ms\n", t);
+  t = time_it([&] { hipLaunchKernelGGL(enc_var<4>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 10);
+  printf("cast+lift   %.3f ms\n", t);
+  {
+    int per_cu = 0, cus = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)enc_pipe, 256, lds));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    for (int mult = 1; mult <= 2; mult++) {
+      dim3 pg((unsigned)(per_cu * cus * mult));
+      t = time_it([&] { hipLaunchKernelGGL(enc_pipe, pg, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 10);
+      printf("pipelined   %.3f ms  (%d groups/CU x %d CUs x %d)  %.0f GB/s(alg)\n", t, per_cu, cus, mult, gb / t * 1e3);
+    }
+    // check: same stream as the one-shot kernel
+    std::vector<uint64_t> a(N / 4), b2(N / 4);
+    hipLaunchKernelGGL(enc_var<0>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic);
+    CK(hipMemcpy(a.data(), o, N * 2, hipMemcpyDeviceToHost));
+    hipLaunchKernelGGL(enc_pipe, dim3(per_cu * cus), block, lds, 0, d, g, cp, o, sw, swp, magic);
+    CK(hipMemcpy(b2.data(), o, N * 2, hipMemcpyDeviceToHost));
+    printf("pipelined stream identical: %s\n", a == b2 ? "yes" : "NO");
+  }
   return 0;
 }

@@ -49,10 +49,11 @@ def main():
     ap.add_argument("--decode", action="store_true")
     ap.add_argument("--dims", type=int, default=3)
     ap.add_argument("--host", action="store_true", help="field and stream in host memory (PCIe-inclusive)")
+    ap.add_argument("--lib", default=R + "/zfp-par_amd/lib/libzfp.so", help="libzfp.so to load (variant builds)")
     a = ap.parse_args()
     import torch
     from capi import ZfpCAPI
-    api = ZfpCAPI(R + "/zfp-par_amd/lib/libzfp.so")
+    api = ZfpCAPI(a.lib)
     api.enable_index()
     lib = api.lib
     dev = torch.device("cuda", 0)

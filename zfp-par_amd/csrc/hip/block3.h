@@ -354,6 +354,8 @@ __device__ __forceinline__ uint32_t encode_ints3(OrSlot& w, const uint32_t* lut,
   if constexpr (HI && PREC == 64) {
     uint32_t Pl[32], Ph[32];
     planes_hi(Pl, Ph, q);
+    pin_registers(Pl);
+    pin_registers(Ph);
     return code_planes<32, PLIM>(w, lut, pos, lim, prec, Pl, Ph);
   } else {
     uint32_t Pl[PREC], Ph[PREC];
@@ -361,6 +363,8 @@ __device__ __forceinline__ uint32_t encode_ints3(OrSlot& w, const uint32_t* lut,
       planes_from_coeffs(Pl, Ph, q);
     else
       planes_from_coeffs(Pl, Ph, q, prec > 32);
+    pin_registers(Pl);
+    pin_registers(Ph);
     return code_planes<PREC, PLIM>(w, lut, pos, lim, prec, Pl, Ph);
   }
 }
@@ -374,11 +378,13 @@ __device__ __forceinline__ uint32_t decode_ints3(WordReader& r, const uint32_t* 
   if constexpr (HI && PREC == 64) {
     uint64_t P[32];
     const uint32_t used = decode_planes64<32, false>(r, sq, budget, prec, P);
+    pin_registers(P);
     coeffs_from_planes_hi(q, P);
     return used;
   } else {
     uint64_t P[PREC];
     uint32_t used = decode_planes64<PREC>(r, sq, budget, prec, P);
+    pin_registers(P);
     if constexpr (PREC == 32)
       coeffs_from_planes(q, P);
     else
@@ -435,6 +441,55 @@ __device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], double (&v)[64]
   mp = precision3(emax, cp);
   fwd_cast(q, v, emax);
   return emax;
+}
+
+// Scheduling fence between the phases of a block (cast, lift, planes, coder):
+// without it the scheduler interleaves neighbouring phases, which keeps both
+// phases' registers live and costs occupancy.
+#ifndef ZFP_PHASE_FENCE
+#define ZFP_PHASE_FENCE 1
+#endif
+#if ZFP_PHASE_FENCE && defined(__HIP_DEVICE_COMPILE__)
+#define ZFP_PHASE_BARRIER() __builtin_amdgcn_sched_barrier(0)
+#else
+#define ZFP_PHASE_BARRIER() ((void)0)
+#endif
+
+// Fixed-rate block (maxprec >= intprec, minbits == maxbits): encodef.c:63-90 +
+// encode.c:260-280 with every lane on one control path.  An all-zero block
+// (e == 0: the single bit "0", then padding) runs the transform and the coder
+// like the others with its position pinned at the budget end, so its bits all
+// land in the slot's spare words and its block stays "0" + zeros.  `mid` runs
+// once the block's bit planes are built and the field values are dead: the
+// pipelined kernel issues the next batch's loads there, so they fly during the
+// coder.
+template <typename S, typename Reload, typename Mid>
+__device__ __forceinline__ void encode_block3_fixed(OrSlot& w, const uint32_t* lut, S (&v)[64], const CodecParams& cp,
+                                                    Reload&& reload, Mid&& mid)
+{
+  using T = Traits<S>;
+  using Int = typename T::Int;
+  constexpr int PREC = T::kIntPrec;
+  constexpr uint32_t kE = T::kEbits;
+  Int q[64];
+  uint32_t mp;
+  const int emax = lossy_emax_cast(q, v, cp, mp, reload);
+  const uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
+  if (e)
+    w.head(2 * e + 1);
+  ZFP_PHASE_BARRIER();
+  xform<3, false, false>(q);
+  ZFP_PHASE_BARRIER();
+  uint32_t Pl[PREC], Ph[PREC];
+  if constexpr (PREC == 32)
+    planes_from_coeffs(Pl, Ph, q);
+  else
+    planes_from_coeffs(Pl, Ph, q, true);
+  ZFP_PHASE_BARRIER();
+  pin_registers(Pl);
+  pin_registers(Ph);
+  mid();
+  code_planes<PREC, false>(w, lut, e ? 1 + kE : cp.maxbits, cp.maxbits, mp, Pl, Ph);
 }
 
 // Encode one block into a zeroed slot; returns its length in bits including
@@ -503,6 +558,10 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
     return bits + ib;
   } else {
     // lossy (encodef.c:63-90)
+    if constexpr (FR && !HI) {
+      encode_block3_fixed(w, lut, v, cp, reload, [] {});
+      return cp.maxbits;
+    }
     uint32_t mp;
     const int emax = lossy_emax_cast(q, v, cp, mp, reload);
     const uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;

@@ -472,6 +472,8 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
       planes_from_coeffs<false>(Pl, Ph, q);
     else
       planes_from_coeffs<false>(Pl, Ph, q, prec > 32);
+    pin_registers(Pl);
+    pin_registers(Ph);
     const uint32_t end = code_planes4<PREC>(d, jmax, lut, bits + T::kPbits, cp.maxbits, prec, Pl, Ph);
     uint32_t ib = end - bits;
     if (ib < minb) ib = minb;
@@ -493,6 +495,8 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
         planes_from_coeffs<false>(Pl, Ph, q);
       else
         planes_from_coeffs<false>(Pl, Ph, q, mp > 32);
+      pin_registers(Pl);
+      pin_registers(Ph);
       uint32_t ib = code_planes4<PREC>(d, jmax, lut, bits, cp.maxbits, mp, Pl, Ph) - bits;
       if (ib < minb) ib = minb;
       bits += ib;
@@ -541,6 +545,7 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
     }
     uint64_t P[PREC];
     decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+    pin_registers(P);
     if constexpr (PREC == 32)
       coeffs_from_planes<false>(q, P);
     else

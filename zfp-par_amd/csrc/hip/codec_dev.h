@@ -160,6 +160,19 @@ __device__ __forceinline__ uint32_t dbl16(const uint32_t* lut, uint32_t u)
   return lut[b0] | (lut[b1] << (8u + (uint32_t)__popc(b0)));
 }
 
+// Materialise every element at this point: the IR passes cannot sink the
+// computation of these values into later (branchy) code, e.g. the last
+// transpose steps into the plane coder, which would keep their inputs live.
+template <typename U, int N>
+__device__ __forceinline__ void pin_registers(U (&a)[N])
+{
+#ifdef __HIP_DEVICE_COMPILE__
+#pragma unroll
+  for (int i = 0; i < N; i++)
+    asm volatile("" : "+v"(a[i]));
+#endif
+}
+
 // Bit reader over a word array in LDS (or global memory).
 struct WordReader {
   const uint64_t* w;

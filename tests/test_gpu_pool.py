@@ -73,8 +73,10 @@ def test_repeated_zfp_parallel_is_exact_and_memory_flat(product, ref_capi):
     ref_back = np.zeros(SHAPE, dtype=np.float32)
     with ThreadPool(8) as pool:
         pool.starmap(lambda s, b: _ref_decode_chunk(ref_capi, s, ref_back, b), zip(want, boxes))
+    orig = a.copy()
     free = []
     for it in range(3):
+        a[...] = orig  # the previous iteration left the decompressed (lossy) field here
         streams = zp.compress(nthreads=8, rate=RATE)
         assert [bytes(s) == w for s, w in zip(streams, want)] == [True] * 8, it
         a[...] = 0

@@ -287,6 +287,28 @@ size_t zfp_decompress_chunk(zfp_stream* stream, const zfp_chunk* chunk, zfp_fiel
 size_t zfp_write_header(zfp_stream* stream, const zfp_field* field, uint mask);
 size_t zfp_read_header(zfp_stream* stream, zfp_field* field, uint mask);
 
+/* ---- the fork's "blocks" API: chunk streams + offset header (zfp.h:714-868) ---- */
+zfp_streams* zfp_streams_alloc(const int nstreams);
+void zfp_streams_free(zfp_streams* streams);
+zfp_streams* zfp_create_streams(const zfp_stream* zfp_in, const int nblocks, const size_t* blocks_boundaries);
+zfp_streams* zfp_blocks_portions(zfp_stream* stream, const zfp_field* field, const int nthreads, zfp_blocks* blocks,
+                                 size_t initial_pos);
+size_t zfp_write_blocks_header(zfp_stream* stream, const zfp_field* field, const zfp_blocks* blocks,
+                               const int begs_after_header);
+size_t zfp_read_blocks_header(zfp_stream* stream, zfp_field* field, zfp_blocks* blocks);
+zfp_streams* zfp_blocks_compress(zfp_stream* stream, const zfp_field* field, const int nthreads,
+                                 const float blocks_per_chunk, const int method, const int begs_after_header);
+zfp_streams* zfp_blocks_compress_multi(zfp_stream* stream, const zfp_field* field, const int nthreads,
+                                       const float blocks_per_chunk, const int method);
+size_t zfp_blocks_compress_single_stream(zfp_stream* stream, const zfp_field* field, const int nthreads,
+                                         const float blocks_per_chunk, const int method);
+size_t zfp_blocks_compress_internal(zfp_stream* stream, const zfp_field* field, const int nthreads,
+                                    zfp_blocks* blocks);
+size_t zfp_blocks_decompress(zfp_stream* stream, zfp_field* field, const int nthreads, const zfp_blocks* blocks);
+size_t zfp_blocks_decompress_multi_stream(zfp_stream* stream, zfp_field* field, zfp_streams* streams,
+                                          const int nthreads);
+size_t zfp_blocks_decompress_single_stream(zfp_stream* stream, zfp_field* field, const int nthreads);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,6 +29,11 @@ class ZfpField(ctypes.Structure):
                 ("sx", pd), ("sy", pd), ("sz", pd), ("sw", pd), ("data", vp)]
 
 
+class ZfpBlocks(ctypes.Structure):
+    """zfp_blocks layout: zfp.h:158-162."""
+    _fields_ = [("bx", sz), ("by", sz), ("bz", sz), ("bw", sz), ("nbeg", i32), ("begs", ctypes.POINTER(sz))]
+
+
 class ZfpCAPI:
     _SIGS = {
         "zfp_stream_open": (vp, [vp]),
@@ -93,6 +98,17 @@ class ZfpCAPI:
         "stream_pad": (None, [vp, u64]),
         "stream_skip": (None, [vp, u64]),
         "stream_rseek": (None, [vp, u64]),
+        "stream_data": (vp, [vp]),
+        "zfp_stream_bit_stream": (vp, [vp]),
+        "zfp_blocks_alloc": (vp, []),
+        "zfp_alloc_nblocks": (None, [vp, sz]),
+        "zfp_write_blocks_header": (sz, [vp, vp, vp, i32]),
+        "zfp_read_blocks_header": (sz, [vp, vp, vp]),
+        "zfp_blocks_compress_single_stream": (sz, [vp, vp, i32, ctypes.c_float, i32]),
+        "zfp_blocks_decompress_single_stream": (sz, [vp, vp, i32]),
+        "zfp_blocks_compress_multi": (vp, [vp, vp, i32, ctypes.c_float, i32]),
+        "zfp_blocks_decompress_multi_stream": (sz, [vp, vp, vp, i32]),
+        "zfp_streams_free": (None, [vp]),
         "stream_wseek": (None, [vp, u64]),
     }
 
@@ -224,6 +240,35 @@ class ZfpCAPI:
         if not self.lib.zfp_hip_last_scan(ctypes.byref(ms), ctypes.byref(passes)):
             return None
         return ms.value, passes.value
+
+    def blocks_single_stream(self, arr, mode, param, blocks_per_chunk, method=1, ztype=None):
+        """zfp_blocks_compress_single_stream: the library allocates the output
+        buffer and installs it as the stream's bit stream (zfp.c:2037-2114)."""
+        if ztype is None:
+            ztype = TYPE_OF[arr.dtype]
+        field = self.field_for(arr)
+        zs = self.lib.zfp_stream_open(None)
+        self.set_mode(zs, mode, param, ztype, arr.ndim)
+        n = self.lib.zfp_blocks_compress_single_stream(zs, field, 4, ctypes.c_float(blocks_per_chunk), method)
+        bs = self.lib.zfp_stream_bit_stream(zs)
+        data = ctypes.string_at(self.lib.stream_data(bs), n) if n else b""
+        self.lib.zfp_stream_close(zs)
+        self.lib.zfp_field_free(field)
+        return data  # (the library's buffer is leaked, as with the reference)
+
+    def blocks_decompress_single_stream(self, data, out):
+        buf = np.frombuffer(bytes(data) + bytes(64), dtype=np.uint8)
+        bs = self.lib.stream_open(buf.ctypes.data, len(data))
+        zs = self.lib.zfp_stream_open(bs)
+        field = self.lib.zfp_field_alloc()
+        self.lib.zfp_field_set_pointer(field, out.ctypes.data)
+        n = self.lib.zfp_blocks_decompress_single_stream(zs, field, 4)
+        f = ctypes.cast(field, ctypes.POINTER(ZfpField)).contents
+        meta = (f.type, f.nx, f.ny, f.nz, f.nw)
+        self.lib.zfp_field_free(field)
+        self.lib.zfp_stream_close(zs)
+        self.lib.stream_close(bs)
+        return n, meta
 
     def make_chunk(self, ndim, box):
         """box: list of (f, e) per zfp axis (x first)."""

@@ -43,6 +43,15 @@ PRODUCT_SO = os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so")
 
 
 @pytest.fixture(scope="session")
+def prod():
+    """The product library for host-only (no GPU) checks."""
+    if not os.path.exists(PRODUCT_SO):
+        pytest.fail("product library not built")
+    from capi import ZfpCAPI
+    return ZfpCAPI(PRODUCT_SO)
+
+
+@pytest.fixture(scope="session")
 def product():
     """The product library; GPU tests fail loudly if it or the GPU is missing."""
     if not os.path.exists(PRODUCT_SO):

@@ -1,0 +1,78 @@
+"""The fork's "blocks" API (src/zfp.c:1651-1797, :1880-2177; no reference test
+covers it -- SURVEY §4 -- so parity is against the reference library itself,
+oracle/_ref, built from the reference sources): a single stream holding a blocks
+header with the chunk bit offsets (`begs`) followed by the word-flushed chunk
+streams.  With the offsets in the wire format, variable-rate chunks decode
+independently after a save/load.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from capi import ZfpBlocks
+
+
+def _field(shape, dtype, seed=1):
+    rng = np.random.default_rng(seed)
+    g = np.indices(shape).sum(axis=0)
+    return (np.sin(0.1 * g) + 0.01 * rng.standard_normal(shape)).astype(dtype)
+
+
+def test_blocks_header_bytes_and_roundtrip_match_reference(prod, ref_capi):
+    """CPU only: header writer/reader against the reference's, for a 3-chunk partition."""
+    out = {}
+    for name, api in (("ref", ref_capi), ("prod", prod)):
+        lib = api.lib
+        arr = np.zeros((9, 10, 11), np.float32)
+        field = api.field_for(arr)
+        zs = lib.zfp_stream_open(None)
+        lib.zfp_stream_set_precision(zs, 20)
+        blk = ZfpBlocks(bx=1, by=1, bz=3, bw=0, nbeg=3)
+        begs = (ctypes.c_size_t * 4)(0, 640, 1920, 4096)
+        blk.begs = ctypes.cast(begs, ctypes.POINTER(ctypes.c_size_t))
+        buf = np.zeros(4096, np.uint8)
+        bs = lib.stream_open(buf.ctypes.data, buf.size)
+        lib.zfp_stream_set_bit_stream(zs, bs)
+        bits = lib.zfp_write_blocks_header(zs, field, ctypes.byref(blk), 1)
+        size = lib.stream_size(bs)
+        out[name] = (bits, bytes(buf[:size]))
+        # read it back
+        lib.zfp_stream_rewind(zs)
+        f2 = lib.zfp_field_alloc()
+        b2 = ZfpBlocks()
+        rbits = lib.zfp_read_blocks_header(zs, f2, ctypes.byref(b2))
+        got = [b2.begs[i] for i in range(b2.nbeg + 1)]
+        assert rbits == bits - 56 and b2.nbeg == 3 and (b2.bx, b2.by, b2.bz) == (1, 1, 3)
+        assert got == [bits + x for x in (0, 640, 1920, 4096)]
+        assert lib.stream_rtell(bs) == bits
+        lib.zfp_field_free(f2)
+        lib.stream_close(bs)
+        lib.zfp_stream_close(zs)
+        lib.zfp_field_free(field)
+    assert out["prod"] == out["ref"]
+
+
+CASES = [((40, 48, 64), np.float32, "precision", 16, 8),
+         ((40, 48, 64), np.float32, "rate", 8, 4),
+         ((33, 33, 33), np.float64, "precision", 32, 8),
+         ((24, 20, 16, 12), np.float32, "reversible", None, 6),
+         ((48, 48, 48), np.float32, "accuracy", 1e-3, 27)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,dtype,mode,param,nparts", CASES)
+def test_single_stream_matches_reference(product, ref_capi, shape, dtype, mode, param, nparts):
+    arr = _field(shape, dtype)
+    nblocks = np.prod([(n + 3) // 4 for n in shape])
+    cpb = nblocks / nparts
+    want = ref_capi.blocks_single_stream(arr, mode, param, cpb)
+    got = product.blocks_single_stream(arr, mode, param, cpb)
+    assert len(got) == len(want) and got == want
+    # decode the reference's bytes (a "file"): chunk offsets come from the header
+    ref_out = np.zeros_like(arr)
+    n_ref, meta_ref = ref_capi.blocks_decompress_single_stream(want, ref_out)
+    out = np.zeros_like(arr)
+    n, meta = product.blocks_decompress_single_stream(want, out)
+    assert (n, meta) == (n_ref, meta_ref)
+    assert out.tobytes() == ref_out.tobytes()

@@ -18,13 +18,6 @@ PRODUCT_SO = os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so")
 HIP_SO = os.path.join(REPO, "zfp-par_amd", "lib", "libzfp_hip.so")
 
 
-@pytest.fixture(scope="module")
-def prod():
-    if not os.path.exists(PRODUCT_SO):
-        pytest.fail("product library not built")
-    return ZfpCAPI(PRODUCT_SO)
-
-
 def _declared(header):
     text = open(os.path.join(REPO, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)

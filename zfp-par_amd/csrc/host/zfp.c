@@ -1172,3 +1172,316 @@ size_t zfp_read_header(zfp_stream* zfp, zfp_field* field, uint mask)
   }
   return bits;
 }
+
+/* ------------------------------------------------------------------------ */
+/* the fork's "blocks" API: chunk streams at offsets recorded in a header    */
+/* (zfp.c:1651-1701 write, :1747-1797 read, :1880-2177 compress/decompress). */
+/* In the reference these run one OpenMP thread per chunk; here every chunk  */
+/* is one zfp_compress_chunk / zfp_decompress_chunk call on the GPU (a       */
+/* variable-rate chunk without an index is found by the GPU stream scan), so */
+/* `nthreads` is accepted and unused.                                        */
+
+zfp_streams* zfp_streams_alloc(const int nstreams)
+{
+  zfp_streams* z = (zfp_streams*)malloc(sizeof(zfp_streams));
+  if (!z)
+    return NULL;
+  z->nstreams = nstreams > 0 ? nstreams : 0;
+  z->streams = (zfp_stream**)calloc(z->nstreams ? (size_t)z->nstreams : 1, sizeof(zfp_stream*));
+  return z;
+}
+
+/* closes each sub-stream's bitstream and zfp_stream (not the shared buffer) */
+void zfp_streams_free(zfp_streams* z)
+{
+  if (!z)
+    return;
+  for (int i = 0; i < z->nstreams; i++)
+    if (z->streams[i]) {
+      stream_close(z->streams[i]->stream);
+      zfp_stream_close(z->streams[i]);
+    }
+  free(z->streams);
+  free(z);
+}
+
+/* sub-stream i over bits [b[i], b[i+1]) of zfp_in's buffer, byte-addressed as
+ * the reference does (b[i] / 8), with zfp_in's codec parameters */
+zfp_streams* zfp_create_streams(const zfp_stream* zfp_in, const int nblocks, const size_t* b)
+{
+  zfp_streams* z = zfp_streams_alloc(nblocks);
+  if (!z)
+    return NULL;
+  stream_rewind(zfp_in->stream);
+  for (int i = 0; i < nblocks; i++) {
+    bitstream* s = stream_open((uchar*)stream_data(zfp_in->stream) + b[i] / 8, b[i + 1] / 8 - b[i] / 8);
+    z->streams[i] = zfp_stream_open(s);
+    zfp_stream_set_params(z->streams[i], zfp_in->minbits, zfp_in->maxbits, zfp_in->maxprec, zfp_in->minexp);
+    if (zfp_in->exec.policy == zfp_exec_hip)
+      zfp_stream_set_hip_device(z->streams[i], stream_device(zfp_in));
+  }
+  return z;
+}
+
+/* Compress every chunk of `blocks` into its own sub-stream; chunk i is given
+ * zfp_stream_maximum_size_chunk bytes starting at bit begs[i] (begs[0] =
+ * initial_pos), flushed.  zfp.c:1914-1938. */
+zfp_streams* zfp_blocks_portions(zfp_stream* stream, const zfp_field* field, const int nthreads, zfp_blocks* blocks,
+                                 size_t initial_pos)
+{
+  int nsize[4];
+  int ndims = zfp_field_to_n(field, nsize);
+  zfp_chunks* chunks = zfp_chunks_from_blocks(ndims, nsize, blocks);
+  zfp_streams* z;
+  (void)nthreads;
+  if (!chunks)
+    return NULL;
+  blocks->begs[0] = initial_pos;
+  for (size_t i = 0; i < chunks->nchunks; i++)
+    blocks->begs[i + 1] = blocks->begs[i] + CHAR_BIT * zfp_stream_maximum_size_chunk(stream, field, chunks->chunks[i]);
+  z = zfp_create_streams(stream, (int)chunks->nchunks, blocks->begs);
+  for (size_t i = 0; z && i < chunks->nchunks; i++) {
+    zfp_compress_chunk(z->streams[i], chunks->chunks[i], field);
+    stream_flush(z->streams[i]->stream);
+  }
+  zfp_chunks_free(chunks);
+  return z;
+}
+
+/* Blocks header: magic, type (8 bits), nx..nw (32 bits each), the 64-bit mode
+ * word, nbeg and bx..bw (32 bits each), nbeg+1 offsets of 64 bits; begs are
+ * stored plus the header's size when begs_after_header == 1; flushed to a
+ * word (the reference's 56-bit pad).  zfp.c:1651-1701. */
+size_t zfp_write_blocks_header(zfp_stream* zfp, const zfp_field* field, const zfp_blocks* blocks,
+                               const int begs_after_header)
+{
+  size_t bits = 0, use_offset = 0;
+  stream_write_bits(zfp->stream, 'z', 8);
+  stream_write_bits(zfp->stream, 'f', 8);
+  stream_write_bits(zfp->stream, 'p', 8);
+  stream_write_bits(zfp->stream, zfp_codec_version, 8);
+  bits += ZFP_MAGIC_BITS;
+  stream_write_bits(zfp->stream, (uint64)field->type, 8);
+  stream_write_bits(zfp->stream, (uint64)field->nx, 32);
+  stream_write_bits(zfp->stream, (uint64)field->ny, 32);
+  stream_write_bits(zfp->stream, (uint64)field->nz, 32);
+  stream_write_bits(zfp->stream, (uint64)field->nw, 32);
+  bits += 136;
+  stream_write_bits(zfp->stream, zfp_stream_mode(zfp), 64); /* always the long form */
+  bits += 64;
+  stream_write_bits(zfp->stream, (uint64)blocks->nbeg, 32);
+  stream_write_bits(zfp->stream, (uint64)blocks->bx, 32);
+  stream_write_bits(zfp->stream, (uint64)blocks->by, 32);
+  stream_write_bits(zfp->stream, (uint64)blocks->bz, 32);
+  stream_write_bits(zfp->stream, (uint64)blocks->bw, 32);
+  bits += 160;
+  bits += 64 * (size_t)(blocks->nbeg + 1) + 56;
+  if (begs_after_header == 1)
+    use_offset = bits;
+  for (int i = 0; i < blocks->nbeg + 1; i++)
+    stream_write_bits(zfp->stream, (uint64)(use_offset + blocks->begs[i]), 64);
+  stream_flush(zfp->stream);
+  return bits;
+}
+
+/* zfp.c:1747-1797: fills field type/extents and the partition (begs is
+ * allocated here), leaves the stream after the 56-bit pad */
+size_t zfp_read_blocks_header(zfp_stream* zfp, zfp_field* field, zfp_blocks* blocks)
+{
+  size_t bits = 0;
+  uint64 mode;
+  if (stream_read_bits(zfp->stream, 8) != 'z' || stream_read_bits(zfp->stream, 8) != 'f' ||
+      stream_read_bits(zfp->stream, 8) != 'p' || stream_read_bits(zfp->stream, 8) != zfp_codec_version)
+    return 0;
+  bits += ZFP_MAGIC_BITS;
+  field->type = (zfp_type)stream_read_bits(zfp->stream, 8);
+  field->nx = (size_t)stream_read_bits(zfp->stream, 32);
+  field->ny = (size_t)stream_read_bits(zfp->stream, 32);
+  field->nz = (size_t)stream_read_bits(zfp->stream, 32);
+  field->nw = (size_t)stream_read_bits(zfp->stream, 32);
+  bits += 136;
+  mode = stream_read_bits(zfp->stream, 64);
+  bits += 64;
+  if (zfp_stream_set_mode(zfp, mode) == zfp_mode_null)
+    return 0;
+  blocks->nbeg = (int)stream_read_bits(zfp->stream, 32);
+  blocks->bx = (size_t)stream_read_bits(zfp->stream, 32);
+  blocks->by = (size_t)stream_read_bits(zfp->stream, 32);
+  blocks->bz = (size_t)stream_read_bits(zfp->stream, 32);
+  blocks->bw = (size_t)stream_read_bits(zfp->stream, 32);
+  bits += 160;
+  free(blocks->begs);
+  blocks->begs = (size_t*)malloc(sizeof(size_t) * (size_t)(blocks->nbeg + 1));
+  if (!blocks->begs)
+    return 0;
+  for (int i = 0; i < blocks->nbeg + 1; i++)
+    blocks->begs[i] = (size_t)stream_read_bits(zfp->stream, 64);
+  bits += 64 * (size_t)(blocks->nbeg + 1);
+  stream_rseek(zfp->stream, bits + 56);
+  return bits;
+}
+
+/* zfp.c:2079-2114: partition the field, compress every chunk into a fresh
+ * buffer (it replaces the stream's bit stream, as in the reference; the caller
+ * owns it: stream_data(zfp_stream_bit_stream(stream))), then write the blocks
+ * header at its start.  Returns the chunk sub-streams. */
+zfp_streams* zfp_blocks_compress(zfp_stream* stream, const zfp_field* field, const int nthreads,
+                                 const float blocks_per_chunk, const int method, const int begs_after_header)
+{
+  int n[4] = {0, 0, 0, 0}, per[4] = {1, 1, 1, 1};
+  int ndims = zfp_field_to_n(field, n);
+  zfp_blocks* zb = zfp_optimal_parts_from_size(ndims, n, blocks_per_chunk, method);
+  int nchunks;
+  size_t bufsize;
+  void* buffer;
+  bitstream* dst;
+  zfp_streams* z;
+  if (!zb)
+    return NULL;
+  nchunks = zfp_total_chunks(ndims, zb, per);
+  bufsize = zfp_stream_maximum_size_blocks(stream, field, zb);
+  buffer = malloc(bufsize);
+  if (!buffer) {
+    zfp_blocks_free(zb);
+    return NULL;
+  }
+  dst = stream_open(buffer, bufsize);
+  zfp_stream_set_bit_stream(stream, dst);
+  z = zfp_blocks_portions(stream, field, nthreads, zb, ZFP_HEADER_BLOCKS_MAX_BITS + (size_t)(nchunks + 1) * 64);
+  zb->begs[0] = 0;
+  for (int i = 0; z && i < zb->nbeg; i++) {
+    stream_flush(z->streams[i]->stream);
+    zb->begs[i + 1] = zb->begs[i] + stream_wtell(z->streams[i]->stream);
+  }
+  zfp_write_blocks_header(stream, field, zb, begs_after_header);
+  zfp_blocks_free(zb);
+  return z;
+}
+
+zfp_streams* zfp_blocks_compress_multi(zfp_stream* stream, const zfp_field* field, const int nthreads,
+                                       const float blocks_per_chunk, const int method)
+{
+  return zfp_blocks_compress(stream, field, nthreads, blocks_per_chunk, method, 0);
+}
+
+/* zfp.c:2037-2065: one stream = blocks header + the chunk streams packed after
+ * it in chunk order (each chunk word-flushed); returns its size in bytes */
+size_t zfp_blocks_compress_single_stream(zfp_stream* stream, const zfp_field* field, const int nthreads,
+                                         const float blocks_per_chunk, const int method)
+{
+  zfp_streams* z = zfp_blocks_compress(stream, field, nthreads, blocks_per_chunk, method, 1);
+  bitstream* dst;
+  size_t offset;
+  if (!z)
+    return 0;
+  dst = stream->stream;
+  offset = stream_wtell(dst);
+  for (int i = 0; i < z->nstreams; i++) {
+    size_t bits = stream_wtell(z->streams[i]->stream);
+    stream_rewind(z->streams[i]->stream);
+    stream_copy(dst, z->streams[i]->stream, bits);
+    offset += bits;
+  }
+  stream_wseek(dst, offset);
+  zfp_streams_free(z);
+  return offset / 8;
+}
+
+/* zfp.c:1942-1981, without the reference's misuse of stream_data() as a bit
+ * stream (undefined behaviour there): chunks are compressed at their reserved
+ * offsets from the stream's current byte, then packed after it; begs[] gets
+ * the packed chunk offsets.  Returns the stream size in bytes. */
+size_t zfp_blocks_compress_internal(zfp_stream* stream, const zfp_field* field, const int nthreads, zfp_blocks* blocks)
+{
+  size_t offset, start = stream_wtell(stream->stream);
+  zfp_streams* z = zfp_blocks_portions(stream, field, nthreads, blocks, start);
+  bitstream* dst = zfp_stream_bit_stream(stream);
+  if (!z)
+    return 0;
+  stream_wseek(dst, start);
+  offset = start;
+  for (int i = 0; i < blocks->nbeg; i++) {
+    size_t bits = stream_wtell(z->streams[i]->stream);
+    blocks->begs[i + 1] = blocks->begs[i] + bits;
+    stream_rewind(z->streams[i]->stream);
+    stream_copy(dst, z->streams[i]->stream, bits);
+    offset += bits;
+  }
+  zfp_streams_free(z);
+  return offset / 8;
+}
+
+/* zfp.c:1984-2008: every chunk of `blocks` from sub-streams at begs[] */
+size_t zfp_blocks_decompress(zfp_stream* stream, zfp_field* field, const int nthreads, const zfp_blocks* blocks)
+{
+  int nsize[4];
+  int ndims = zfp_field_to_n(field, nsize);
+  zfp_chunks* chunks = zfp_chunks_from_blocks(ndims, nsize, blocks);
+  zfp_streams* z;
+  size_t val;
+  (void)nthreads;
+  if (!chunks)
+    return 0;
+  z = zfp_create_streams(stream, (int)chunks->nchunks, blocks->begs);
+  for (size_t i = 0; z && i < chunks->nchunks; i++)
+    zfp_decompress_chunk(z->streams[i], chunks->chunks[i], field);
+  zfp_streams_free(z);
+  val = blocks->begs[chunks->nchunks];
+  zfp_chunks_free(chunks);
+  return val / 8;
+}
+
+/* zfp.c:2147-2177: re-reads the header from the start of `stream`, then every
+ * chunk from its sub-stream */
+size_t zfp_blocks_decompress_multi_stream(zfp_stream* stream, zfp_field* field, zfp_streams* zstreams,
+                                          const int nthreads)
+{
+  int nsize[4];
+  zfp_blocks* zb = zfp_blocks_alloc();
+  zfp_chunks* chunks;
+  size_t val;
+  int ndims;
+  (void)nthreads;
+  if (!zb)
+    return 0;
+  stream_rewind(stream->stream);
+  if (!zfp_read_blocks_header(stream, field, zb)) {
+    zfp_blocks_free(zb);
+    return 0;
+  }
+  ndims = zfp_field_to_n(field, nsize);
+  chunks = zfp_chunks_from_blocks(ndims, nsize, zb);
+  for (size_t i = 0; chunks && i < chunks->nchunks && (int)i < zstreams->nstreams; i++) {
+    stream_rewind(zstreams->streams[i]->stream);
+    zfp_decompress_chunk(zstreams->streams[i], chunks->chunks[i], field);
+  }
+  val = zb->begs[zb->nbeg];
+  zfp_chunks_free(chunks);
+  zfp_blocks_free(zb);
+  return val / 8;
+}
+
+/* zfp.c:2116-2145 */
+size_t zfp_blocks_decompress_single_stream(zfp_stream* stream, zfp_field* field, const int nthreads)
+{
+  int nsize[4];
+  zfp_blocks* zb = zfp_blocks_alloc();
+  zfp_chunks* chunks;
+  zfp_streams* z;
+  size_t loc;
+  int ndims;
+  if (!zb)
+    return 0;
+  if (!zfp_read_blocks_header(stream, field, zb)) {
+    zfp_blocks_free(zb);
+    return 0;
+  }
+  ndims = zfp_field_to_n(field, nsize);
+  chunks = zfp_chunks_from_blocks(ndims, nsize, zb);
+  z = zfp_create_streams(stream, (int)(chunks ? chunks->nchunks : 0), zb->begs);
+  loc = z ? zfp_blocks_decompress_multi_stream(stream, field, z, nthreads) : 0;
+  zfp_chunks_free(chunks);
+  zfp_blocks_free(zb);
+  zfp_streams_free(z);
+  return loc;
+}

@@ -13,6 +13,18 @@ import pytest
 from capi import ZfpBlocks
 
 
+def _mask_bw(data, ndim):
+    """For ndim < 4 the reference header's 32-bit `bw` field (bits 360..391) is
+    whatever malloc left in zfp_blocks.bw (zfp_optimal_parts_from_size never
+    sets it, zfp.c:669-794); this library writes 0.  Compare without it."""
+    if ndim >= 4:
+        return data
+    w = np.frombuffer(bytes(data), dtype=np.uint64).copy()
+    w[5] &= np.uint64((1 << 40) - 1)
+    w[6] &= ~np.uint64(0xff)
+    return w.tobytes()
+
+
 def _field(shape, dtype, seed=1):
     rng = np.random.default_rng(seed)
     g = np.indices(shape).sum(axis=0)
@@ -68,7 +80,7 @@ def test_single_stream_matches_reference(product, ref_capi, shape, dtype, mode, 
     cpb = nblocks / nparts
     want = ref_capi.blocks_single_stream(arr, mode, param, cpb)
     got = product.blocks_single_stream(arr, mode, param, cpb)
-    assert len(got) == len(want) and got == want
+    assert len(got) == len(want) and _mask_bw(got, arr.ndim) == _mask_bw(want, arr.ndim)
     # decode the reference's bytes (a "file"): chunk offsets come from the header
     ref_out = np.zeros_like(arr)
     n_ref, meta_ref = ref_capi.blocks_decompress_single_stream(want, ref_out)

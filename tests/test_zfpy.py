@@ -109,12 +109,10 @@ def _gather_worker(rank, world, port, nchunks, q):
     try:
         local = {}
         for i in zdist.rank_chunks(nchunks, world, rank):
-            s = zfpy.zfpy_c.ZfpBytes(bytes([i % 251]) * (100 + 37 * i))
-            s.block_index = (b"idx%d" % i) if i % 3 else None
-            local[i] = s
+            local[i] = zfpy.zfpy_c.ZfpBytes(bytes([i % 251]) * (100 + 37 * i))
         out = zdist.gather_streams(local, nchunks, dst=0)
         if rank == 0:
-            q.put([(bytes(s), s.block_index) for s in out])
+            q.put([bytes(s) for s in out])
         else:
             q.put(out)
     finally:
@@ -141,9 +139,8 @@ def test_gather_streams_gloo_world2():
     assert len(root) == 1 and res.count(None) == 1
     got = root[0]
     assert len(got) == nchunks
-    for i, (s, idx) in enumerate(got):
+    for i, s in enumerate(got):
         assert s == bytes([i % 251]) * (100 + 37 * i)
-        assert idx == ((b"idx%d" % i) if i % 3 else None)
 
 
 # ---------------- CPU: header() ----------------

@@ -5,12 +5,23 @@ chunk's blocks, `_zfp_par.py` / `pyx:330-376`), so the compression itself needs
 no collective.  Chunk i is compressed by rank i % world on that rank's GPU.
 The only exchange is handing every chunk stream to the root, in chunk order:
 an all-reduce of the per-chunk sizes, then one gather of each rank's
-concatenated payload (RCCL over xGMI with the "nccl" backend and device
-tensors; gloo with host tensors in the CPU tests).  Variable-rate streams carry
-their GPU block index (`ZfpBytes.block_index`), which travels the same way.
+concatenated payload.
+
+  nccl (RCCL over xGMI): each chunk is compressed straight into a device
+        buffer (the stream's header words are written through hipMemcpy by the
+        host library), the payloads are gathered device to device, and only
+        the root copies the streams to host bytes -- the chunk never crosses
+        PCIe on the compressing rank.
+  gloo (CPU tests): host bytes, as the single-process zfp_parallel returns.
+
+Variable-rate streams need no side-band data: the decoder finds the block
+starts itself (zfp_hip_index_build).
 """
+import ctypes
+
 import numpy as np
 
+from . import zfpy_c
 from .zfpy_c import ZfpBytes
 
 
@@ -21,64 +32,86 @@ def rank_chunks(nchunks, world, rank):
 
 def _device_for(dist, group):
     import torch
-    backend = dist.get_backend(group)
-    if backend == "nccl":
+    if dist.get_backend(group) == "nccl":
         return torch.device("cuda", torch.cuda.current_device())
     return torch.device("cpu")
 
 
-def gather_streams(local, nchunks, dst=0, group=None):
-    """Gather {chunk id: bytes} from every rank to `dst`.
+def _sizes(local, nchunks, dev, dist, group):
+    import torch
+    sizes = torch.zeros(nchunks, dtype=torch.int64, device=dev)
+    for i, s in local.items():
+        sizes[i] = s.numel() if hasattr(s, "numel") else len(s)
+    dist.all_reduce(sizes, op=dist.ReduceOp.SUM, group=group)
+    return sizes.cpu().numpy()
 
-    Returns the list of all chunk streams in chunk order on `dst` (each a
-    ZfpBytes with its block_index restored), None elsewhere.  Two collectives:
-    all_reduce of the per-chunk (stream, index) sizes, gather of the payloads
-    padded to the largest rank payload.
-    """
+
+def gather_streams(local, nchunks, dst=0, group=None):
+    """Gather {chunk id: stream} from every rank to `dst`; returns the list of all
+    chunk streams (bytes) in chunk order on `dst`, None elsewhere.  A stream is
+    host bytes, or a uint8 device tensor on the nccl path (gathered in HBM)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = _device_for(dist, group)
-
-    sizes = torch.zeros(2 * nchunks, dtype=torch.int64, device=dev)
-    for i, s in local.items():
-        sizes[2 * i] = len(s)
-        blob = getattr(s, "block_index", None)
-        sizes[2 * i + 1] = len(blob) if blob else 0
-    dist.all_reduce(sizes, op=dist.ReduceOp.SUM, group=group)
-    sz = sizes.cpu().numpy().reshape(nchunks, 2)
-
-    per_rank = [int(sz[rank_chunks(nchunks, world, r)].sum()) if nchunks else 0 for r in range(world)]
+    sz = _sizes(local, nchunks, dev, dist, group)
+    per_rank = [int(sz[rank_chunks(nchunks, world, r)].sum()) for r in range(world)]
     mx = max(per_rank) if per_rank else 0
-    payload = np.zeros(mx, dtype=np.uint8)
-    off = 0
+    pieces = []
     for i in rank_chunks(nchunks, world, rank):
-        s = bytes(local[i])
-        payload[off:off + len(s)] = np.frombuffer(s, dtype=np.uint8)
-        off += len(s)
-        blob = getattr(local[i], "block_index", None) or b""
-        if blob:
-            payload[off:off + len(blob)] = np.frombuffer(blob, dtype=np.uint8)
-        off += len(blob)
-    send = torch.from_numpy(payload).to(dev)
+        s = local[i]
+        pieces.append(s.to(dev) if isinstance(s, torch.Tensor) else
+                      torch.from_numpy(np.frombuffer(bytes(s), dtype=np.uint8).copy()).to(dev))
+    if per_rank[rank] < mx:
+        pieces.append(torch.zeros(mx - per_rank[rank], dtype=torch.uint8, device=dev))
+    send = torch.cat(pieces) if pieces else torch.zeros(mx, dtype=torch.uint8, device=dev)
     recv = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == dst else None
     dist.gather(send, gather_list=recv, dst=dst, group=group)
     if rank != dst:
         return None
-
     out = [None] * nchunks
     for r in range(world):
-        buf = recv[r].cpu().numpy().tobytes()
+        buf = recv[r].cpu().numpy().tobytes()  # one device-to-host copy per rank payload, on the root
         off = 0
         for i in rank_chunks(nchunks, world, r):
-            n_s, n_b = int(sz[i, 0]), int(sz[i, 1])
-            s = ZfpBytes(buf[off:off + n_s])
-            off += n_s
-            s.block_index = buf[off:off + n_b] if n_b else None
-            off += n_b
-            out[i] = s
+            n = int(sz[i])
+            out[i] = ZfpBytes(buf[off:off + n])
+            off += n
     return out
+
+
+def compress_chunk_to_device(zp, ichunk, tolerance=-1, rate=-1, precision=-1, device=None):
+    """compress_numpy_portion with the stream in HBM: returns a uint8 device
+    tensor holding the chunk stream (whole-field header + the chunk's blocks),
+    byte-identical to compress_numpy_portion's bytes."""
+    import torch
+    lib = zfpy_c._lib
+    ck = zp.get_chunkit()
+    dev = torch.device("cuda", torch.cuda.current_device() if device is None else device)
+    field = zfpy_c._init_field_raw(zp.get_raw_array(), ck)
+    stream = lib.zfp_stream_open(None)
+    bstream = None
+    try:
+        lib.zfp_stream_set_hip_device(stream, dev.index)
+        zfpy_c._set_compression_mode(stream, zfpy_c.type_none, ck.ndim, tolerance, rate, precision)
+        cp = ck.chunk_ptr(ichunk)
+        cap = lib.zfp_stream_maximum_size_chunk(stream, field, cp) + (zfpy_c.HEADER_MAX_BITS + 63) // 64 * 8 + 8
+        buf = torch.zeros(cap, dtype=torch.uint8, device=dev)
+        bstream = lib.stream_open(ctypes.c_void_p(buf.data_ptr()), cap)
+        lib.zfp_stream_set_bit_stream(stream, bstream)
+        lib.zfp_stream_rewind(stream)
+        if lib.zfp_write_header(stream, field, zfpy_c.HEADER_FULL) == 0:
+            raise RuntimeError("Failed to write header to stream")
+        n = lib.zfp_compress_chunk(stream, cp, field)
+        if n == 0:
+            raise RuntimeError("Failed to write to stream")
+        return buf[:n]
+    finally:
+        lib.zfp_field_free(field)
+        lib.zfp_stream_close(stream)
+        if bstream:
+            lib.stream_close(bstream)
 
 
 def compress_distributed(zp, tolerance=-1, rate=-1, precision=-1, dst=0, group=None):
@@ -87,15 +120,17 @@ def compress_distributed(zp, tolerance=-1, rate=-1, precision=-1, dst=0, group=N
     (stored in zp._compress_data there, as the single-process compress does)."""
     import torch
     import torch.distributed as dist
-
-    from .zfpy_c import compress_numpy_portion
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     ck = zp.get_chunkit()
     n = ck.get_nchunks()
-    device = torch.cuda.current_device() if torch.cuda.is_available() else -1
-    local = {i: compress_numpy_portion(zp.get_raw_array(), ck, i, tolerance, rate, precision, device=device)
-             for i in rank_chunks(n, world, rank)}
+    mine = rank_chunks(n, world, rank)
+    if dist.get_backend(group) == "nccl":
+        local = {i: compress_chunk_to_device(zp, i, tolerance, rate, precision) for i in mine}
+    else:
+        device = torch.cuda.current_device() if torch.cuda.is_available() else -1
+        local = {i: zfpy_c.compress_numpy_portion(zp.get_raw_array(), ck, i, tolerance, rate, precision,
+                                                  device=device) for i in mine}
     streams = gather_streams(local, n, dst=dst, group=group)
     if streams is not None:
         zp._compress_data = streams

@@ -142,6 +142,130 @@ __global__ __launch_bounds__(256, KEXP_PIPE_WPS) void enc_pipe(const float* __re
   }
 }
 
+
+// persistent (one batch at a time, no prefetch) with an optional start stagger
+// so the load phases of the waves sharing a SIMD fall at different times
+template <int STAGGER>
+__global__ __launch_bounds__(256, 4) void enc_persist(const float* __restrict__ data, Geometry g, CodecParams cp,
+                                                    uint64_t* __restrict__ out, uint32_t sw, uint32_t swp, uint32_t magic)
+{
+  __shared__ uint32_t lut[256];
+  extern __shared__ uint64_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint64_t* wslot = lds + (size_t)wv * 64 * swp;
+  lut[threadIdx.x] = dbl_entry(threadIdx.x);
+  __syncthreads();
+  const uint64_t nw = (g.nblocks + 63) / 64;
+  const uint64_t step = (uint64_t)gridDim.x * kWavesPerGroup;
+  uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  if (STAGGER) {
+    const uint32_t h = (blockIdx.x * 2654435761u) >> 29;  // 0..7
+    for (uint32_t i = 0; i < h * STAGGER; i++)
+      __builtin_amdgcn_s_sleep(127);
+  }
+  uint64_t* slot = wslot + (size_t)lane * swp;
+  for (; w < nw; w += step) {
+    for (uint32_t i = 0; i + 1 < swp; i += 2)
+      *reinterpret_cast<ulonglong2*>(slot + i) = make_ulonglong2(0, 0);
+    slot[swp - 1] = 0;
+    const uint64_t b = w * 64 + lane;
+    if (b < g.nblocks) {
+      float v[64];
+      const BlockPos p = block_pos(g, b, 3);
+      gather3<float, true>(v, data, g, p);
+      OrSlot os{slot, 2 * swp - 1};
+      encode_block3_fixed(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); }, [] {});
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = 64 * sw;
+    uint64_t* dst = out + w * 64 * sw;
+    for (uint32_t i = 2 * lane; i < total; i += 128) {
+      const uint32_t l = div_magic(i, magic);
+      const uint64_t* src = wslot + (size_t)l * swp + (i - l * sw);
+      ulonglong2 q; q.x = src[0]; q.y = src[1];
+      *reinterpret_cast<ulonglong2*>(dst + i) = q;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+
+// persistent, prefetching the first two z-slabs (8 float4 = 32 VGPRs) of the
+// next batch while the current one is coded; 96 + 32 VGPRs keeps 4 waves/SIMD
+__global__ __launch_bounds__(256, 4) void enc_half(const float* __restrict__ data, Geometry g, CodecParams cp,
+                                                  uint64_t* __restrict__ out, uint32_t sw, uint32_t swp, uint32_t magic)
+{
+  __shared__ uint32_t lut[256];
+  extern __shared__ uint64_t lds[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint64_t* wslot = lds + (size_t)wv * 64 * swp;
+  lut[threadIdx.x] = dbl_entry(threadIdx.x);
+  __syncthreads();
+  const uint64_t nw = (g.nblocks + 63) / 64;
+  const uint64_t step = (uint64_t)gridDim.x * kWavesPerGroup;
+  uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  uint64_t* slot = wslot + (size_t)lane * swp;
+  const int64_t sy = g.s[1], sz = g.s[2];
+  float4 pre[8];
+  if (w < nw) {
+    const float* o = data + block_pos(g, w * 64 + lane, 3).off;
+#pragma unroll
+    for (int k = 0; k < 2; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) pre[4 * k + j] = *reinterpret_cast<const float4*>(o + j * sy + k * sz);
+  }
+  for (; w < nw; w += step) {
+    for (uint32_t i = 0; i + 1 < swp; i += 2)
+      *reinterpret_cast<ulonglong2*>(slot + i) = make_ulonglong2(0, 0);
+    slot[swp - 1] = 0;
+    const uint64_t b = w * 64 + lane;
+    const uint64_t wn = w + step;
+    float v[64];
+    const BlockPos p = block_pos(g, b, 3);
+    {
+      const float* o = data + p.off;
+#pragma unroll
+      for (int k = 2; k < 4; k++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          float4 q = *reinterpret_cast<const float4*>(o + j * sy + k * sz);
+          v[16 * k + 4 * j] = q.x; v[16 * k + 4 * j + 1] = q.y; v[16 * k + 4 * j + 2] = q.z; v[16 * k + 4 * j + 3] = q.w;
+        }
+#pragma unroll
+      for (int k = 0; k < 2; k++)
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          float4 q = pre[4 * k + j];
+          v[16 * k + 4 * j] = q.x; v[16 * k + 4 * j + 1] = q.y; v[16 * k + 4 * j + 2] = q.z; v[16 * k + 4 * j + 3] = q.w;
+        }
+    }
+    OrSlot os{slot, 2 * swp - 1};
+    encode_block3_fixed(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); },
+                        [&] {
+                          if (wn < nw) {
+                            const float* o = data + block_pos(g, wn * 64 + lane, 3).off;
+#pragma unroll
+                            for (int k = 0; k < 2; k++)
+#pragma unroll
+                              for (int j = 0; j < 4; j++) pre[4 * k + j] = *reinterpret_cast<const float4*>(o + j * sy + k * sz);
+                          }
+                        });
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t total = 64 * sw;
+    uint64_t* dst = out + w * 64 * sw;
+    for (uint32_t i = 2 * lane; i < total; i += 128) {
+      const uint32_t l = div_magic(i, magic);
+      const uint64_t* src = wslot + (size_t)l * swp + (i - l * sw);
+      ulonglong2 q; q.x = src[0]; q.y = src[1];
+      *reinterpret_cast<ulonglong2*>(dst + i) = q;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 template <typename K>
 static float time_it(K launch, int reps)
 {
@@ -157,9 +281,10 @@ static float time_it(K launch, int reps)
   return ms / reps;
 }
 
-int main()
+int main(int argc, char** argv)
 {
   setvbuf(stdout, nullptr, _IOLBF, 0);
+  const bool quick = argc > 1;
   const uint64_t n = 1024;
   const size_t N = n * n * n;
   float* d; uint64_t* o;
@@ -186,6 +311,29 @@ int main()
   float t;
   t = time_it([&] { hipLaunchKernelGGL(enc_var<0>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 10);
   printf("full        %.3f ms  %.0f GB/s(alg)\n", t, gb / t * 1e3);
+  if (quick) {
+    int per_cu = 0, cus = 0;
+    CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, (const void*)enc_persist<0>, 256, lds));
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    dim3 pg((unsigned)(per_cu * cus));
+    for (int r = 0; r < 3; r++) {
+      t = time_it([&] { hipLaunchKernelGGL(enc_var<0>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 20);
+      printf("one-shot      %.3f ms\n", t);
+      t = time_it([&] { hipLaunchKernelGGL(enc_persist<0>, pg, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 20);
+      printf("persist       %.3f ms (%d/CU)\n", t, per_cu);
+      t = time_it([&] { hipLaunchKernelGGL(enc_half, pg, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 20);
+      printf("persist+half  %.3f ms\n", t);
+      t = time_it([&] { hipLaunchKernelGGL(enc_persist<2>, pg, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 20);
+      printf("persist+stag2 %.3f ms\n", t);
+    }
+    std::vector<uint64_t> a(N / 4), b2(N / 4);
+    hipLaunchKernelGGL(enc_var<0>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic);
+    CK(hipMemcpy(a.data(), o, N * 2, hipMemcpyDeviceToHost));
+    hipLaunchKernelGGL(enc_half, pg, block, lds, 0, d, g, cp, o, sw, swp, magic);
+    CK(hipMemcpy(b2.data(), o, N * 2, hipMemcpyDeviceToHost));
+    printf("persist stream identical: %s\n", a == b2 ? "yes" : "NO");
+    return 0;
+  }
   t = time_it([&] { hipLaunchKernelGGL(enc_var<1>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 10);
   printf("no-coder    %.3f ms\n", t);
   t = time_it([&] { hipLaunchKernelGGL(enc_var<2>, grid, block, lds, 0, d, g, cp, o, sw, swp, magic); }, 10);

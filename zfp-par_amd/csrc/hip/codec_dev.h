@@ -510,6 +510,9 @@ __device__ __forceinline__ void expand_event(OrSlot& s, const uint32_t* lut, con
 // budget keep going with their position pinned at lim, so their bits land in
 // the slot's spare words and no per-lane predication is needed.  PLIM = true:
 // a lane stops at its precision limit, so its state is updated under `act`.
+#ifndef ZFP_FR_EXIT_PLANES
+#define ZFP_FR_EXIT_PLANES 16
+#endif
 template <int PREC, bool PLIM>
 __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, uint32_t pos, uint32_t lim,
                                                 uint32_t maxprec, const uint32_t (&Pl)[PREC],
@@ -528,7 +531,11 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
 #endif
   for (int k = PREC - 1; k >= 0; k--) {
     const bool act = p31 < lim31 && (!PLIM || (uint32_t)k >= kmin);
-    if (__builtin_amdgcn_ballot_w64(act) == 0)
+    // wave-level exit once every lane is done; without a precision limit
+    // (fixed rate) only the low planes are checked: a block rarely spends
+    // its budget in fewer planes, and each check is a VALU->SALU->branch
+    // round trip
+    if ((PLIM || k < ZFP_FR_EXIT_PLANES) && __builtin_amdgcn_ballot_w64(act) == 0)
       break;
     const uint32_t pl = Pl[k], ph = Ph[k];
     const uint32_t Nl = pl & ~Sl, Nh = ph & ~Sh;

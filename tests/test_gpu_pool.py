@@ -75,7 +75,7 @@ def test_repeated_zfp_parallel_is_exact_and_memory_flat(product, ref_capi):
         pool.starmap(lambda s, b: _ref_decode_chunk(ref_capi, s, ref_back, b), zip(want, boxes))
     orig = a.copy()
     free = []
-    for it in range(3):
+    for it in range(4):
         a[...] = orig  # the previous iteration left the decompressed (lossy) field here
         streams = zp.compress(nthreads=8, rate=RATE)
         assert [bytes(s) == w for s, w in zip(streams, want)] == [True] * 8, it
@@ -84,5 +84,8 @@ def test_repeated_zfp_parallel_is_exact_and_memory_flat(product, ref_capi):
         assert np.array_equal(a, ref_back), it
         torch.cuda.synchronize()
         free.append(torch.cuda.mem_get_info()[0])
-    # the first call sizes the pooled scratch; later calls reuse it
-    assert free[1] == free[2] and abs(free[0] - free[1]) < (64 << 20), free
+    # the first call sizes the pooled scratch; later calls reuse it.  Which
+    # pooled context serves which chunk depends on thread timing, so a context
+    # may still grow a small buffer by a size class; a leaked context would
+    # hold at least one chunk's staging (256 MiB).
+    assert min(free[1:]) > free[0] - (64 << 20), free

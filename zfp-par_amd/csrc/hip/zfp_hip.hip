@@ -152,7 +152,13 @@ static int ensure(Scratch& s, size_t bytes)
   if (s.bytes >= bytes)
     return 1;
   free_scratch(s);
-  size_t want = std::max(bytes, (size_t)4096);
+  // size classes (powers of two up to 256 MiB, then 64 MiB steps): calls of
+  // slightly different sizes reuse a context's buffers instead of regrowing them
+  size_t want = 64 << 10;
+  if (bytes > ((size_t)256 << 20))
+    want = (bytes + ((size_t)64 << 20) - 1) & ~(((size_t)64 << 20) - 1);
+  else
+    while (want < bytes) want <<= 1;
   hipError_t e = hipMalloc(&s.p, want);
   if (e != hipSuccess) {
     s.p = nullptr;
@@ -174,7 +180,7 @@ static Ctx* acquire_ctx(int device)
   }
   {
     std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (size_t i = 0; i < g_idle.size(); i++)
+    for (size_t i = g_idle.size(); i-- > 0;)  // most recently returned first
       if (g_idle[i]->device == device) {
         Ctx* c = g_idle[i];
         g_idle.erase(g_idle.begin() + (long)i);

@@ -30,6 +30,16 @@ static inline uint32_t __builtin_amdgcn_alignbit(uint32_t a, uint32_t b, uint32_
 {
   return (uint32_t)((((uint64_t)a << 32) | b) >> (c & 31));
 }
+// v_bitop3_b32: result bit = ttbl bit (s0 << 2 | s1 << 1 | s2) of the inputs' bits
+static inline uint32_t __builtin_amdgcn_bitop3_b32(uint32_t s0, uint32_t s1, uint32_t s2, uint32_t ttbl)
+{
+  uint32_t r = 0;
+  for (int i = 0; i < 32; i++) {
+    uint32_t idx = (((s0 >> i) & 1u) << 2) | (((s1 >> i) & 1u) << 1) | ((s2 >> i) & 1u);
+    r |= ((ttbl >> idx) & 1u) << i;
+  }
+  return r;
+}
 // v_perm_b32: bytes 0-3 from src1, 4-7 from src0
 static inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel)
 {

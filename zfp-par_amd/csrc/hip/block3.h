@@ -184,6 +184,7 @@ __device__ __forceinline__ void scatter3(const S (&v)[64], S* __restrict__ base,
 }
 
 // ---- coefficient order + negabinary, then bit planes ----
+// Negabinary: nb_planes / transpose32_nb (codec_dev.h).
 // Planes as two 32-bit halves: Pl[k] bit i = plane k of coefficient i (i < 32),
 // Ph[k] bit i = plane k of coefficient 32 + i.  P3: q is in raster order and is
 // read through kPerm3 (3D); false: q is already in coding order (a 4D lane's
@@ -193,11 +194,11 @@ __device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[32], uint32_t 
 {
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    Pl[i] = ((uint32_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
-    Ph[i] = ((uint32_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaau) ^ 0xaaaaaaaau;
+    Pl[i] = nb_planes((uint32_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaau);
+    Ph[i] = nb_planes((uint32_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaau);
   }
-  transpose32(Pl);
-  transpose32(Ph);
+  transpose32_nb(Pl);
+  transpose32_nb(Ph);
 }
 
 // double: planes 32..63 from the high words; 0..31 only when `need_low`
@@ -208,13 +209,13 @@ __device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[64], uint32_t 
   uint32_t a[32], b[32];
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    uint64_t u0 = ((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
-    uint64_t u1 = ((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    uint64_t u0 = nb_planes((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull);
+    uint64_t u1 = nb_planes((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull);
     a[i] = (uint32_t)(u0 >> 32);
     b[i] = (uint32_t)(u1 >> 32);
   }
-  transpose32(a);
-  transpose32(b);
+  transpose32_nb(a);
+  transpose32_nb(b);
 #pragma unroll
   for (int k = 0; k < 32; k++) {
     Pl[32 + k] = a[k];
@@ -223,13 +224,13 @@ __device__ __forceinline__ void planes_from_coeffs(uint32_t (&Pl)[64], uint32_t 
   if (__any(need_low)) {
 #pragma unroll
     for (int i = 0; i < 32; i++) {
-      uint64_t u0 = ((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
-      uint64_t u1 = ((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+      uint64_t u0 = nb_planes((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull);
+      uint64_t u1 = nb_planes((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull);
       a[i] = (uint32_t)u0;
       b[i] = (uint32_t)u1;
     }
-    transpose32(a);
-    transpose32(b);
+    transpose32_nb(a);
+    transpose32_nb(b);
 #pragma unroll
     for (int k = 0; k < 32; k++) {
       Pl[k] = a[k];
@@ -303,13 +304,13 @@ __device__ __forceinline__ void planes_hi(uint32_t (&Pl)[32], uint32_t (&Ph)[32]
 {
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    uint64_t u0 = ((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
-    uint64_t u1 = ((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull) ^ 0xaaaaaaaaaaaaaaaaull;
+    uint64_t u0 = nb_planes((uint64_t)q[P3 ? kPerm3[i] : i] + 0xaaaaaaaaaaaaaaaaull);
+    uint64_t u1 = nb_planes((uint64_t)q[P3 ? kPerm3[i + 32] : i + 32] + 0xaaaaaaaaaaaaaaaaull);
     Pl[i] = (uint32_t)(u0 >> 32);
     Ph[i] = (uint32_t)(u1 >> 32);
   }
-  transpose32(Pl);
-  transpose32(Ph);
+  transpose32_nb(Pl);
+  transpose32_nb(Ph);
 }
 
 // twin of planes_hi: coefficients from planes 32..63 (low planes zero)

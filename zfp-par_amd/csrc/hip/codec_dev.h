@@ -406,13 +406,26 @@ __device__ __forceinline__ void xform(Int (&p)[1 << (2 * D)])
   }
 }
 
+// Negabinary is u = (x + K) ^ K with K = 0xaa..a (encode.c:67-71).  The XOR
+// only inverts the odd bit planes, so the encoders transpose x + K and invert
+// the odd planes in the transpose's last step, where the inversion is free
+// (a three-input bit operation either way).
+#ifndef ZFP_NB_FOLD
+#define ZFP_NB_FOLD 1
+#endif
+template <typename U>
+__device__ __forceinline__ U nb_planes(U x)
+{
+  return ZFP_NB_FOLD ? x : x ^ (U)0xaaaaaaaaaaaaaaaaull;
+}
+
 // ---------------------------------------------------------------------------
 // Bit-matrix transpose of 32x32 bits held in 32 registers: a[r] bit c <-> a[c] bit r.
 // Used both ways: coefficients -> bit planes (encode) and back (decode).
 // ---------------------------------------------------------------------------
 // Byte-granular steps are one v_perm_b32 per output word, the rest one shift
 // plus one v_bfi_b32.
-template <int J>
+template <int J, bool INV_ODD = false>
 __device__ __forceinline__ void transpose_step(uint32_t (&a)[32])
 {
   constexpr uint32_t M = (J == 4) ? 0x0f0f0f0fu : (J == 2) ? 0x33333333u : 0x55555555u;
@@ -429,7 +442,10 @@ __device__ __forceinline__ void transpose_step(uint32_t (&a)[32])
       a[k | J] = __builtin_amdgcn_perm(y, x, 0x07030501u);
     } else {
       a[k] = (x & M) | ((y << J) & ~M);
-      a[k | J] = ((x >> J) & M) | (y & ~M);
+      if constexpr (INV_ODD)  // ~(x >> J ? M : y) as one v_bitop3 (the compiler would split it)
+        a[k | J] = __builtin_amdgcn_bitop3_b32(x >> J, y, M, 0x1b);
+      else
+        a[k | J] = ((x >> J) & M) | (y & ~M);
     }
   }
 }
@@ -441,6 +457,16 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32])
   transpose_step<4>(a);
   transpose_step<2>(a);
   transpose_step<1>(a);
+}
+
+// encoder: coefficients x + K -> negabinary bit planes (odd planes inverted)
+__device__ __forceinline__ void transpose32_nb(uint32_t (&a)[32])
+{
+  transpose_step<16>(a);
+  transpose_step<8>(a);
+  transpose_step<4>(a);
+  transpose_step<2>(a);
+  transpose_step<1, ZFP_NB_FOLD != 0>(a);
 }
 
 // ---------------------------------------------------------------------------
@@ -470,7 +496,9 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32])
 //
 // Group units 1..3 of a plane whose top one lies past bit 15 of xs (h >= 16):
 // at most three such planes per block (each makes >= 17 coefficients
-// significant).  The coder records them and expands them after the plane loop.
+// significant).  The 32-plane coder expands them where they occur, in a
+// wave-uniform branch; the 64-plane coder records them and expands them after
+// the plane loop.
 struct ExtEvent {
   uint32_t gp;      // slot position of the plane's group bits
   uint32_t xl, xh;  // xs
@@ -513,6 +541,20 @@ __device__ __forceinline__ void expand_event(OrSlot& s, const uint32_t* lut, con
 #ifndef ZFP_FR_EXIT_PLANES
 #define ZFP_FR_EXIT_PLANES 16
 #endif
+// x >> 5 hidden from the optimizer, which would otherwise rewrite the dword
+// address (x >> 5) * 4 + base as ((x >> 3) & ~3) + base: three operations
+// instead of a shift and a v_lshl_add_u32
+__device__ __forceinline__ uint32_t opaque_shr5(uint32_t x)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+  uint32_t r;
+  asm("v_lshrrev_b32 %0, 5, %1" : "=v"(r) : "v"(x));
+  return r;
+#else
+  return x >> 5;
+#endif
+}
+
 template <int PREC, bool PLIM>
 __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, uint32_t pos, uint32_t lim,
                                                 uint32_t maxprec, const uint32_t (&Pl)[PREC],
@@ -523,7 +565,7 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
   const uint32_t lim31 = lim + 31u;
   uint32_t p31 = pos + 31u;  // position + 31: j = p31 >> 5, alignbit shift = 31 - p31
   uint32_t n = 0, nn = ~0u, Sl = 0, Sh = 0;
-  ExtEvent e0{0, 0, 0, 0}, e1{0, 0, 0, 0}, e2{0, 0, 0, 0};
+  ExtEvent e0{0, 0, 0, 0}, e1{0, 0, 0, 0}, e2{0, 0, 0, 0};  // PREC > 32 only
 #ifdef ZFP_PLANE_UNROLL
 #pragma unroll ZFP_PLANE_UNROLL
 #else
@@ -549,20 +591,40 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
     const uint64_t xs = N >> (n & 63u);  // n == 64 only with N == 0
     const uint32_t x0 = (uint32_t)xs;
     const uint32_t b0 = x0 & 0xffu;
-    const uint32_t d16 = lut[b0] | (lut[(x0 >> 8) & 0xffu] << (8u + (uint32_t)__popc(b0)));
+    const uint32_t sh1 = 8u + (uint32_t)__popc(b0);
+    // the table reads fly while the verbatim bits and the rare branch below
+    // are issued; the doubled-ones unit d16 is assembled where it is used
+    const uint32_t l0 = lut[b0], l1 = lut[(x0 >> 8) & 0xffu];
     const uint32_t m = (2u | impl) << ((t2 + nn) & 31u);  // surplus of the top pair at h + c
-    uint32_t g = ((d16 << 1) | (nz ? 1u : 0u)) - m;
     const uint32_t h = n1 + nn;  // top one of xs (when nz)
     const bool ext = act && nz && h >= 16u;
+    const int32_t dlen = (int32_t)t2 + 1 + ((int32_t)(uint32_t)(S1 >> 32) >> 31) + ((int32_t)Nh >> 31);
+    if (!PLIM) {
+      uint32_t* q = dm1 + opaque_shr5(p31);
+      const uint32_t t = 31u - p31;
+      const uint32_t v0 = pl ^ Nl, v1 = ph ^ Nh;  // the n verbatim bits
+      lds_or32(q, __builtin_amdgcn_alignbit(v0, 0u, t));
+      lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
+      lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
+    }
     if (__builtin_amdgcn_ballot_w64(ext) != 0) {
-      if (ext) {
-        g += m;  // the top pair is not in unit 0
+      const uint32_t g32 = (l1 << sh1) >> 31;  // bit 31 of d16: bit 32 of the plane's group bits
+      const ExtEvent e{p31 - 31u + n, x0, (uint32_t)(xs >> 32), h | (impl << 6) | (g32 << 7)};
+      if constexpr (PREC <= 32) {
+        // rare (a few planes per wave): the lanes whose top one lies past
+        // unit 0 write their remaining group units now, the others take no part
+        expand_event(s, lut, ExtEvent{e.gp, e.xl, e.xh, ext ? e.hb : 0u});
+      } else if (ext) {
+        // 64 planes: the inline expansion would keep the plane loop from
+        // being unrolled, so the (at most three) events are expanded after it
         e2 = e1;
         e1 = e0;
-        e0 = ExtEvent{p31 - 31u + n, x0, (uint32_t)(xs >> 32), h | (impl << 6) | ((d16 >> 31) << 7)};
+        e0 = e;
       }
     }
-    const int32_t dlen = (int32_t)t2 + 1 + ((int32_t)(uint32_t)(S1 >> 32) >> 31) + ((int32_t)Nh >> 31);
+    const uint32_t d16 = l0 | (l1 << sh1);
+    // the top pair's surplus is in unit 0 unless the top one lies past it
+    const uint32_t g = ((d16 << 1) | (nz ? 1u : 0u)) - (ext ? 0u : m);
     if (PLIM) {
       if (act) {
         s.put64(p31 - 31u, pl ^ Nl, ph ^ Nh);  // the n verbatim bits
@@ -573,21 +635,11 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
       Sl = act ? (uint32_t)S1 : Sl;
       Sh = act ? (uint32_t)(S1 >> 32) : Sh;
     } else {
-      {
-        uint32_t* q = dm1 + (p31 >> 5);
-        const uint32_t t = 31u - p31;
-        const uint32_t v0 = pl ^ Nl, v1 = ph ^ Nh;
-        lds_or32(q, __builtin_amdgcn_alignbit(v0, 0u, t));
-        lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
-        lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
-      }
-      {
-        const uint32_t pg = p31 + n;
-        uint32_t* q = dm1 + (pg >> 5);
-        const uint32_t t = 31u - pg;
-        lds_or32(q, __builtin_amdgcn_alignbit(g, 0u, t));
-        lds_or32(q + 1, __builtin_amdgcn_alignbit(0u, g, t));
-      }
+      const uint32_t pg = p31 + n;
+      uint32_t* q = dm1 + opaque_shr5(pg);
+      const uint32_t t = 31u - pg;
+      lds_or32(q, __builtin_amdgcn_alignbit(g, 0u, t));
+      lds_or32(q + 1, __builtin_amdgcn_alignbit(0u, g, t));
       p31 += (uint32_t)dlen;
       p31 = p31 < lim31 ? p31 : lim31;
       n = n1;
@@ -596,12 +648,14 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
     }
     nn = ~n;
   }
-  if (__any(e0.hb >= 16u)) {
-    expand_event(s, lut, e0);
-    if (__any(e1.hb >= 16u)) {
-      expand_event(s, lut, e1);
-      if (__any(e2.hb >= 16u))
-        expand_event(s, lut, e2);
+  if constexpr (PREC > 32) {
+    if (__any(e0.hb >= 16u)) {
+      expand_event(s, lut, e0);
+      if (__any(e1.hb >= 16u)) {
+        expand_event(s, lut, e1);
+        if (__any(e2.hb >= 16u))
+          expand_event(s, lut, e2);
+      }
     }
   }
   const uint32_t end = p31 - 31u;

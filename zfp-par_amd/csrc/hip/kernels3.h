@@ -163,13 +163,17 @@ constexpr uint64_t kStAgg = 1ull << 62;
 constexpr uint64_t kStIncl = 2ull << 62;
 constexpr uint64_t kStMask = (1ull << 62) - 1;
 
-// Decoupled look-back (single-pass chained scan): each wave publishes its
-// aggregate, walks back over predecessors' status words until an inclusive
-// prefix, publishes its own inclusive prefix.  Status words are the data
-// (one 8-byte agent-scope atomic store/load each), so no separate flag or
-// fence is needed; waves take tickets in launch order so every awaited wave
-// is already running.  Spins are bounded (error flag on timeout).
-__device__ __forceinline__ uint64_t lookback(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
+// Decoupled look-back (single-pass chained scan, lookback_wave below): each
+// wave publishes its aggregate, walks back over predecessors' status words
+// until an inclusive prefix, publishes its own inclusive prefix.  Status words
+// are the data (one 8-byte agent-scope atomic store/load each), so no separate
+// flag or fence is needed; waves take tickets in launch order so every awaited
+// wave is already running.  Spins are bounded (error flag on timeout).
+
+// One lane walks back (lane 0 returns the prefix).  The f64 encoders keep this
+// form: their waves are few and slow, a predecessor has nearly always published
+// its inclusive prefix, and the wave-wide window measured slower there (C3).
+__device__ __forceinline__ uint64_t lookback_lane(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
 {
   uint64_t excl = 0;
   if (w == 0) {
@@ -180,8 +184,8 @@ __device__ __forceinline__ uint64_t lookback(uint64_t* status, uint64_t w, uint3
   uint64_t j = w - 1;
   uint32_t spins = 0;
   for (;;) {
-    uint64_t st = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t tag = st & ~kStMask;
+    const uint64_t st = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t tag = st & ~kStMask;
     if (tag == 0) {
       if (++spins > (1u << 26)) {
         atomicOr(error, 1u);
@@ -196,6 +200,62 @@ __device__ __forceinline__ uint64_t lookback(uint64_t* status, uint64_t w, uint3
     j--;
   }
   __hip_atomic_store(&status[w], kStIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return excl;
+}
+
+// wave-wide sum of a 64-bit value
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x)
+{
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1)
+    x += __shfl_xor(x, d, 64);
+  return x;
+}
+
+// The look-back runs on the whole wave: lane l inspects predecessor
+// top - l, so one round trip to L2 covers 64 predecessors.  With thousands of
+// waves resident, the predecessors of a wave have mostly published only their
+// aggregates when it looks back (their own look-backs are still walking), and
+// a one-lane walk pays one round trip per predecessor, holding the wave's slots
+// meanwhile; the window makes that chain 64 times shorter.  Called by every
+// lane of the wave with the same arguments.
+__device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  if (w == 0) {
+    if (lane == 0)
+      __hip_atomic_store(&status[0], kStIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&status[w], kStAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t excl = 0;
+  int64_t top = (int64_t)w - 1;
+  uint32_t spins = 0;
+  for (;;) {
+    const int64_t j = top - (int64_t)lane;
+    // before wave 0: an inclusive zero
+    const uint64_t st = j >= 0 ? __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kStIncl;
+    const uint64_t tag = st & ~kStMask;
+    const uint64_t incl = __builtin_amdgcn_ballot_w64(tag == kStIncl);
+    const uint32_t m = incl ? (uint32_t)__builtin_ctzll(incl) : 64u;  // nearest inclusive prefix
+    const uint64_t need = m < 63u ? ((2ull << m) - 1ull) : ~0ull;     // lanes 0 .. m
+    if (__builtin_amdgcn_ballot_w64(tag == 0) & need) {  // a predecessor has not published yet
+      if (++spins > (1u << 24)) {
+        if (lane == 0)
+          atomicOr(error, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    excl += wave_sum64(lane <= m ? (st & kStMask) : 0ull);
+    if (m < 64u)
+      break;
+    top -= 64;
+  }
+  if (lane == 0)
+    __hip_atomic_store(&status[w], kStIncl | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return excl;
 }
 
@@ -251,10 +311,14 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   uint64_t start = 0;  // bit offset of the wave's first block relative to g0
   if (!live) {
   } else if (a.var) {
-    uint64_t e = 0;
-    if (lane == 0)
-      e = lookback(a.status, w, total, a.error);
-    start = __shfl(e, 0, 64);
+    if constexpr (sizeof(S) == 8) {
+      uint64_t e = 0;
+      if (lane == 0)
+        e = lookback_lane(a.status, w, total, a.error);
+      start = __shfl(e, 0, 64);
+    } else {
+      start = lookback_wave(a.status, w, total, a.error);
+    }
     if (a.idx_len && b < g.nblocks)
       a.idx_len[b] = (uint16_t)len;
     if (lane == 0) {
@@ -266,9 +330,11 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   } else {
     start = first * (uint64_t)a.maxbits;
   }
-  __syncthreads();
   if (!live)
     return;
+  // off/wrt and the slots are this wave's own: LDS ops of a wave complete in order
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
   pack_wave<64>(a, wbase, off, wrt, w, start, total);
 }
 

@@ -94,10 +94,7 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   uint64_t start = 0;
   if (!live) {
   } else if (a.var) {
-    uint64_t e = 0;
-    if (lane == 0)
-      e = lookback(a.status, w, total, a.error);
-    start = __shfl(e, 0, 64);
+    start = lookback_wave(a.status, w, total, a.error);
     if (a.idx_len && valid && r == 0u)
       a.idx_len[b] = (uint16_t)len;
     if (lane == 0) {

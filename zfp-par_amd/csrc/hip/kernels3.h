@@ -157,6 +157,7 @@ struct GeneralArgs {
   uint64_t* idx_base;     // per-wave start offsets relative to g0 (optional)
   uint64_t* total_bits;   // written by the last wave (variable rate)
   uint32_t* error;        // look-back timeout flag
+  uint64_t idx_add;       // added to the index bases (offset of this launch in its chunk)
 };
 
 constexpr uint64_t kStAgg = 1ull << 62;
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
       a.idx_len[b] = (uint16_t)len;
     if (lane == 0) {
       if (a.idx_base)
-        a.idx_base[w] = start;
+        a.idx_base[w] = start + a.idx_add;
       if (w == nwaves - 1)
         *a.total_bits = start + total;
     }
@@ -402,15 +403,17 @@ __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* 
 
 // Zero every word that receives partial contributions (the word holding the
 // stream's pending bits below g0 gets those bits instead), then OR them in.
+// `head_keep` selects bits of the head word's current device value to keep
+// (a host slab pipeline: the bits the previous slab wrote below g0).
 __global__ void fixup_zero(const Partial* __restrict__ partials, uint64_t n, uint64_t* out, uint64_t head_idx,
-                           uint64_t head_val)
+                           uint64_t head_val, uint64_t head_keep)
 {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n)
     return;
   uint64_t idx = partials[i].idx;
   if (idx != kNoWord)
-    out[idx] = (idx == head_idx) ? head_val : 0ull;
+    out[idx] = (idx == head_idx) ? ((out[idx] & head_keep) | head_val) : 0ull;
 }
 
 __global__ void fixup_or(const Partial* __restrict__ partials, uint64_t n, uint64_t* out)

@@ -99,7 +99,7 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
       a.idx_len[b] = (uint16_t)len;
     if (lane == 0) {
       if (a.idx_base)
-        a.idx_base[w] = start;
+        a.idx_base[w] = start + a.idx_add;
       if (w == nwaves - 1)
         *a.total_bits = start + total;
     }

@@ -14,11 +14,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
 #include <mutex>
+#include <numeric>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "kernels4.h"
@@ -109,6 +113,7 @@ struct Scratch {
 struct Ctx {
   int device = -1;
   hipStream_t stream = nullptr;
+  hipStream_t side[2] = {nullptr, nullptr};  // host slab pipeline: uploads, downloads
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // [4], [5]: index scan
   Scratch field, words, status, partials, misc;
   Scratch scan_bm, scan_seg, scan_tiles, scan_pos;  // index scan of a stream without index
@@ -144,6 +149,8 @@ static void destroy_ctx(Ctx* c)
     if (e) (void)hipEventDestroy(e);
   if (c->stream)
     (void)hipStreamDestroy(c->stream);
+  for (auto& q : c->side)
+    if (q) (void)hipStreamDestroy(q);
   delete c;
 }
 
@@ -315,6 +322,19 @@ static size_t slot_words_odd(uint32_t bits)
 // ---------------------------------------------------------------------------
 // launchers
 
+// The stream word holding an encode's first bit (bits below g0 belong to what
+// precedes it): `val` ORed in (the host's pending bits), or with `keep` the bits
+// already in the device word are kept (a host slab pipeline: what the previous
+// slab wrote).  `idx_add` is added to the per-wave index bases (the launch's
+// bit offset within its chunk).
+struct Head {
+  uint64_t val = 0;
+  bool keep = false;
+  uint64_t idx_add = 0;
+};
+
+static uint64_t head_keep_mask(const Head& h, uint32_t g0) { return h.keep && g0 ? (1ull << g0) - 1 : 0ull; }
+
 // double with maxprec <= 32: the kernels that code planes 32..63 only
 template <typename S>
 static bool hi_planes(const Plan& p)
@@ -355,7 +375,7 @@ static void launch_decode3(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 bl
 // waves: fix-up partials, look-back state and, for a variable-rate stream with
 // an index, the index buffers.  Queues the look-back resets on the stream.
 static int general_args(Ctx* c, const Plan& p, uint64_t nwaves, uint32_t swp, uint64_t* d_out, uint32_t g0,
-                        zfp_hip_index* index, GeneralArgs& a)
+                        zfp_hip_index* index, uint64_t idx_add, GeneralArgs& a)
 {
   const bool var = !p.fixed;
   // misc: [0] total bits, [1] ticket|error
@@ -373,6 +393,7 @@ static int general_args(Ctx* c, const Plan& p, uint64_t nwaves, uint32_t swp, ui
   a.ticket = (uint32_t*)((char*)c->misc.p + 8);
   a.error = (uint32_t*)((char*)c->misc.p + 12);
   a.partials = (Partial*)c->partials.p;
+  a.idx_add = idx_add;
   if (var && index) {
     if (!index_reserve(index, p.g.nblocks, nwaves))
       return 0;
@@ -392,12 +413,12 @@ static int general_args(Ctx* c, const Plan& p, uint64_t nwaves, uint32_t swp, ui
 
 // After a packing encoder: merge the words shared by neighbouring waves; for a
 // variable-rate stream read back its length (and the look-back health flag).
-static int finish_general(Ctx* c, const Plan& p, uint64_t nwaves, uint64_t* d_out, uint32_t g0, uint64_t head_word,
+static int finish_general(Ctx* c, const Plan& p, uint64_t nwaves, uint64_t* d_out, uint32_t g0, const Head& head,
                           const GeneralArgs& a, zfp_hip_index* index, uint64_t* total_bits)
 {
   unsigned fg = (unsigned)((2 * nwaves + 255) / 256);
   hipLaunchKernelGGL(fixup_zero, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out, 0ull,
-                     g0 ? head_word : 0ull);
+                     g0 ? head.val : 0ull, head_keep_mask(head, g0));
   hipLaunchKernelGGL(fixup_or, dim3(fg), dim3(256), 0, c->stream, a.partials, 2 * nwaves, d_out);
   HIP_TRY(hipGetLastError());
   if (!p.fixed) {
@@ -418,7 +439,7 @@ static int finish_general(Ctx* c, const Plan& p, uint64_t nwaves, uint64_t* d_ou
 // 4D: encode4 for every mode (one 64-thread workgroup per 16 blocks)
 template <typename S>
 static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out, uint32_t g0,
-                          uint64_t head_word, zfp_hip_index* index, uint64_t* total_bits)
+                          const Head& head, zfp_hip_index* index, uint64_t* total_bits)
 {
   using Int = typename Traits<S>::Int;
   const uint64_t nwaves = (p.g.nblocks + kBlocks4PerWave - 1) / kBlocks4PerWave;
@@ -431,7 +452,7 @@ static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_o
   if (lds > 160 * 1024)
     return fail("zfp_hip: 4D block bound %u bits too large for LDS", p.bound_bits);
   GeneralArgs a{};
-  if (!general_args(c, p, nwaves, swp, d_out, g0, index, a))
+  if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
     return 0;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   dim3 grid((unsigned)nwaves), block(64);
@@ -446,15 +467,15 @@ static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_o
     hipLaunchKernelGGL((encode4<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  return finish_general(c, p, nwaves, d_out, g0, head_word, a, index, total_bits);
+  return finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
 }
 
 template <typename S>
 static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out, uint32_t g0,
-                         uint64_t head_word, zfp_hip_index* index, uint64_t* total_bits)
+                         const Head& head, zfp_hip_index* index, uint64_t* total_bits)
 {
   if (p.dims == 4)
-    return launch_encode4<S>(c, p, d_field, d_out, g0, head_word, index, total_bits);
+    return launch_encode4<S>(c, p, d_field, d_out, g0, head, index, total_bits);
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
   if (ngroups > 0x7fffffffull)
@@ -486,7 +507,8 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (g0) {
       unsigned fg = (unsigned)((2 * nwaves + 255) / 256);
-      hipLaunchKernelGGL(fixup_zero, dim3(fg), dim3(256), 0, c->stream, parts, 2 * nwaves, d_out, 0ull, head_word);
+      hipLaunchKernelGGL(fixup_zero, dim3(fg), dim3(256), 0, c->stream, parts, 2 * nwaves, d_out, 0ull, head.val,
+                         head_keep_mask(head, g0));
       hipLaunchKernelGGL(fixup_or, dim3(fg), dim3(256), 0, c->stream, parts, 2 * nwaves, d_out);
       HIP_TRY(hipGetLastError());
     }
@@ -499,7 +521,7 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   if (lds + kLutBytes > 160 * 1024)
     return fail("zfp_hip: block bound %u bits too large for LDS", p.bound_bits);
   GeneralArgs a{};
-  if (!general_args(c, p, nwaves, swp, d_out, g0, index, a))
+  if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
     return 0;
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   if constexpr (sizeof(S) == 8) {
@@ -512,7 +534,7 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  return finish_general(c, p, nwaves, d_out, g0, head_word, a, index, total_bits);
+  return finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
 }
 
 template <typename S>
@@ -617,8 +639,11 @@ static void record_timing(Ctx* c)
 
 // copy the box of elements between a host field and a device image of its
 // span (device pointer d_base corresponds to host pointer h_base)
-static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es, bool to_host)
+static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es, bool to_host,
+                    hipStream_t q = nullptr)
 {
+  if (!q)
+    q = c->stream;
   // whole span contiguous?  (full x/y extents, default strides)
   const Geometry& g = p.g;
   bool contiguous = true;
@@ -641,9 +666,9 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
     size_t off = (size_t)p.span_lo * es;
     size_t bytes = (size_t)(p.span_hi - p.span_lo + 1) * es;
     if (to_host)
-      HIP_TRY(hipMemcpyAsync((char*)h_base + off, (char*)d_base + off, bytes, kind, c->stream));
+      HIP_TRY(hipMemcpyAsync((char*)h_base + off, (char*)d_base + off, bytes, kind, q));
     else
-      HIP_TRY(hipMemcpyAsync((char*)d_base + off, (char*)h_base + off, bytes, kind, c->stream));
+      HIP_TRY(hipMemcpyAsync((char*)d_base + off, (char*)h_base + off, bytes, kind, q));
     return 1;
   }
   if (g.s[0] != 1)
@@ -657,7 +682,7 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
       int64_t off = (int64_t)g.f[0] * g.s[0] + (int64_t)(p.dims >= 2 ? g.f[1] : 0) * (p.dims >= 2 ? g.s[1] : 0) +
                     (int64_t)z * (p.dims >= 3 ? g.s[2] : 0) + (int64_t)w * (p.dims >= 4 ? g.s[3] : 0);
       HIP_TRY(hipMemcpy2DAsync((char*)h_base + off * (int64_t)es, pitch, (char*)d_base + off * (int64_t)es, pitch,
-                               width, rows, kind, c->stream));
+                               width, rows, kind, q));
     }
   return 1;
 }
@@ -803,6 +828,325 @@ static bool index_matches(const zfp_hip_index* x, const Plan& p, uint64_t bit_of
 }
 
 // ---------------------------------------------------------------------------
+// Host-resident field and stream: slab pipeline.  The chunk is
+// cut along its outermost axis into slabs of whole block layers (default about
+// 128 MB of field each).  Three host threads drive three HIP streams:
+//   uploads    field slab s (compress) / stream words of slab s (decompress)
+//   kernels    slab s once its upload is done (a device-side event wait)
+//   downloads  stream words / field slab s once its kernel is done
+// so the two PCIe directions run at once (pageable copies from two threads: 83
+// GB/s together on the box, 57 and 55 alone) and the kernels hide under them.
+// Slab s is an ordinary chunk encode at bit offset O_s: fixed rate O_s is
+// analytic; variable rate O_s = O_{s-1} + its length, known when slab s-1's
+// kernel returns (the look-back runs within a slab).  The word holding O_s is
+// shared by two slabs: slab s keeps the bits slab s-1 left below its first bit
+// (Head::keep), and slab s-1's download stops before that word.  Every slab has
+// its own region of the device images, so no buffer is reused while a copy of
+// it may be in flight.
+static uint64_t env_mb(const char* name, uint64_t dflt)
+{
+  if (const char* e = getenv(name)) {
+    const uint64_t v = strtoull(e, nullptr, 10);
+    if (v)
+      return v << 20;
+  }
+  return dflt << 20;
+}
+
+struct Slab {
+  zfp_hip_job job;
+  Plan p;
+  uint64_t b0;  // first block of the slab within the chunk
+};
+
+// Slabs of whole block layers along the outermost axis; false: the chunk is
+// not worth (or not fit for) the pipeline.  `align`: slabs hold whole waves of
+// this many blocks (variable rate: the chunk's block index layout).
+static bool make_slabs(const zfp_hip_job* job, const void* field_base, const Plan& p, uint64_t align,
+                       std::vector<Slab>& out)
+{
+  const size_t es = p.dbl ? 8 : 4;
+  const uint64_t field_bytes = (uint64_t)(p.span_hi - p.span_lo + 1) * es;
+  if (field_bytes < env_mb("ZFP_HIP_PIPE_MIN_MB", 256))
+    return false;
+  // contiguous layout: each slab's span is its own range of the field
+  int64_t expect = 1;
+  for (int a = 0; a < p.dims; a++) {
+    if (p.g.s[a] != expect)
+      return false;
+    expect *= (int64_t)p.g.n[a];
+  }
+  const int ao = p.dims - 1;
+  const uint64_t nbo = p.g.nb[ao];
+  if (nbo < 2)
+    return false;
+  const uint64_t layer = p.g.nblocks / nbo;
+  const uint64_t layer_bytes = layer * (p.dims == 4 ? 256u : 64u) * es;
+  uint64_t L = std::max<uint64_t>(1, env_mb("ZFP_HIP_PIPE_SLAB_MB", 128) / layer_bytes);
+  if (align > 1) {
+    const uint64_t q = align / std::gcd(layer, align);
+    L = (L + q - 1) / q * q;
+  }
+  if (L >= nbo)
+    return false;
+  for (uint64_t l0 = 0; l0 < nbo; l0 += L) {
+    Slab sl;
+    sl.job = *job;
+    sl.job.f[ao] = job->f[ao] + 4 * l0;
+    sl.job.e[ao] = std::min<uint64_t>(job->e[ao], job->f[ao] + 4 * (l0 + L));
+    if (!plan_job(&sl.job, field_base, sl.p))
+      return false;
+    sl.b0 = l0 * layer;
+    out.push_back(sl);
+  }
+  return true;
+}
+
+static int ensure_side_streams(Ctx* c)
+{
+  for (auto& q : c->side)
+    if (!q)
+      HIP_TRY(hipStreamCreateWithFlags(&q, hipStreamNonBlocking));
+  return 1;
+}
+
+// Hand-off between the pipeline's host threads: `done[k]` counts the slabs
+// whose stage-k event is recorded (a stream can only wait for a recorded event).
+struct PipeSync {
+  std::mutex mu;
+  std::condition_variable cv;
+  size_t done[2] = {0, 0};
+  bool failed = false;
+  std::string err;
+  void post(int k, size_t n)
+  {
+    { std::lock_guard<std::mutex> l(mu); done[k] = n; }
+    cv.notify_all();
+  }
+  void fail_with(const char* what)
+  {
+    { std::lock_guard<std::mutex> l(mu); if (!failed) { failed = true; err = what; } }
+    cv.notify_all();
+  }
+  bool wait(int k, size_t n)  // false: another stage failed
+  {
+    std::unique_lock<std::mutex> l(mu);
+    cv.wait(l, [&] { return failed || done[k] >= n; });
+    return !failed;
+  }
+};
+
+struct EventSet {
+  std::vector<hipEvent_t> ev;
+  explicit EventSet(size_t n) : ev(n, nullptr)
+  {
+    for (auto& e : ev)
+      (void)hipEventCreateWithFlags(&e, hipEventDisableTiming);
+  }
+  ~EventSet()
+  {
+    for (auto& e : ev)
+      if (e) (void)hipEventDestroy(e);
+  }
+};
+
+template <typename S>
+static int compress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, const void* field_base,
+                          uint64_t* words, uint64_t capacity_words, uint64_t bit_offset, uint64_t head_word,
+                          zfp_hip_index* index, uint64_t* end_bit)
+{
+  const size_t es = sizeof(S);
+  const size_t ns = sl.size();
+  const uint64_t W0 = bit_offset >> 6;
+  const uint64_t worst_bits = (bit_offset & 63) + p.g.nblocks * (uint64_t)(p.fixed ? p.cp.maxbits : p.max_len);
+  const uint64_t worst_words = (worst_bits + 63) / 64 + 1;
+  if (!ensure(c->field, (size_t)(p.span_hi - p.span_lo + 1) * es) || !ensure(c->words, worst_words * 8) ||
+      !ensure_side_streams(c))
+    return 0;
+  char* d_img = (char*)c->field.p - p.span_lo * (int64_t)es;
+  uint64_t* d_words = (uint64_t*)c->words.p;
+  const uint32_t per_wave = p.dims == 4 ? kBlocks4PerWave : 64u;
+  const bool var_index = !p.fixed && index;
+  if (var_index && !index_reserve(index, p.g.nblocks, (p.g.nblocks + per_wave - 1) / per_wave))
+    return 0;
+  EventSet ev_in(ns), ev_k(ns);
+  std::vector<uint64_t> wa(ns), wb(ns);  // stream words [wa, wb) of slab s, relative to W0
+  PipeSync ps;
+  std::thread up([&] {
+    if (hipSetDevice(c->device) != hipSuccess)
+      return ps.fail_with("hipSetDevice failed (upload thread)");
+    for (size_t s = 0; s < ns; s++) {
+      if (!copy_box(c, sl[s].p, (void*)field_base, d_img, es, false, c->side[0]) ||
+          hipEventRecord(ev_in.ev[s], c->side[0]) != hipSuccess)
+        return ps.fail_with("field upload failed");
+      ps.post(0, s + 1);
+    }
+  });
+  std::thread down([&] {
+    if (hipSetDevice(c->device) != hipSuccess)
+      return ps.fail_with("hipSetDevice failed (download thread)");
+    for (size_t s = 0; s < ns; s++) {
+      if (!ps.wait(1, s + 1))
+        return;
+      if (hipStreamWaitEvent(c->side[1], ev_k.ev[s], 0) != hipSuccess ||
+          hipMemcpyAsync(words + W0 + wa[s], d_words + wa[s], (wb[s] - wa[s]) * 8, hipMemcpyDeviceToHost,
+                         c->side[1]) != hipSuccess)
+        return ps.fail_with("stream download failed");
+    }
+    if (hipStreamSynchronize(c->side[1]) != hipSuccess)
+      ps.fail_with("stream download failed");
+  });
+  uint64_t off = bit_offset;
+  int ok = 1;
+  for (size_t s = 0; s < ns && ok; s++) {
+    if (!ps.wait(0, s + 1)) {
+      ok = 0;
+      break;
+    }
+    if (hipStreamWaitEvent(c->stream, ev_in.ev[s], 0) != hipSuccess) {
+      ok = fail("hipStreamWaitEvent failed");
+      break;
+    }
+    const uint64_t Ws = off >> 6;
+    Head h;
+    h.val = s == 0 ? head_word : 0ull;
+    h.keep = s > 0;
+    h.idx_add = off - bit_offset;
+    zfp_hip_index view;  // the slab's part of the chunk's index
+    if (var_index) {
+      view.device = c->device;
+      view.d_len = index->d_len + sl[s].b0;
+      view.d_base = index->d_base + sl[s].b0 / per_wave;
+      view.cap_blocks = view.cap_waves = ~(size_t)0;
+    }
+    uint64_t total = 0;
+    ok = launch_encode<S>(c, sl[s].p, (const S*)d_img, d_words + (Ws - W0), (uint32_t)(off & 63), h,
+                          var_index ? &view : nullptr, &total);
+    view.d_len = nullptr;  // a view: nothing to free
+    view.d_base = nullptr;
+    if (!ok)
+      break;
+    const uint64_t next = off + total;
+    wa[s] = Ws - W0;
+    wb[s] = (s + 1 < ns ? next >> 6 : (next + 63) >> 6) - W0;
+    if (W0 + wb[s] > capacity_words) {
+      ok = fail("zfp_hip_compress: compressed stream (%llu words) exceeds capacity %llu",
+                (unsigned long long)(W0 + wb[s]), (unsigned long long)capacity_words);
+      break;
+    }
+    if (hipEventRecord(ev_k.ev[s], c->stream) != hipSuccess) {
+      ok = fail("hipEventRecord failed");
+      break;
+    }
+    ps.post(1, s + 1);
+    off = next;
+  }
+  if (!ok)
+    ps.fail_with(g_err.c_str());
+  up.join();
+  down.join();
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->side[0]);
+  if (!ok)
+    return 0;
+  if (ps.failed)
+    return fail("zfp_hip_compress: %s", ps.err.c_str());
+  if (var_index) {
+    index->device = c->device;
+    index->nblocks = p.g.nblocks;
+    index->nwaves = (p.g.nblocks + per_wave - 1) / per_wave;
+    index->per_wave = per_wave;
+    index->total_bits = off - bit_offset;
+    index->start_bit = bit_offset;
+  }
+  *end_bit = off;
+  return 1;
+}
+
+// fixed rate: slab s's words are known before any kernel runs
+template <typename S>
+static int decompress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, void* field_base,
+                            const uint64_t* words, uint64_t capacity_words, uint64_t bit_offset, uint64_t* end_bit)
+{
+  const size_t es = sizeof(S);
+  const size_t ns = sl.size();
+  const uint64_t W0 = bit_offset >> 6;
+  const uint64_t avail = capacity_words > W0 ? capacity_words - W0 : 0;
+  const uint64_t mb = p.cp.maxbits;
+  const uint64_t nwords = std::min<uint64_t>(((bit_offset & 63) + p.g.nblocks * mb + 63) / 64 + 1, avail);
+  if (!ensure(c->field, (size_t)(p.span_hi - p.span_lo + 1) * es) || !ensure(c->words, nwords * 8 + 8) ||
+      !ensure_side_streams(c))
+    return 0;
+  char* d_img = (char*)c->field.p - p.span_lo * (int64_t)es;
+  uint64_t* d_words = (uint64_t*)c->words.p;
+  EventSet ev_in(ns), ev_k(ns);
+  // stream words [wa, wb) relative to W0 read by slab s (one word of lookahead)
+  std::vector<uint64_t> wa(ns), wb(ns);
+  for (size_t s = 0; s < ns; s++) {
+    const uint64_t o = bit_offset + sl[s].b0 * mb;
+    wa[s] = (o >> 6) - W0;
+    wb[s] = std::min<uint64_t>(((o + sl[s].p.g.nblocks * mb + 63) >> 6) + 1 - W0, nwords);
+  }
+  PipeSync ps;
+  std::thread up([&] {
+    if (hipSetDevice(c->device) != hipSuccess)
+      return ps.fail_with("hipSetDevice failed (upload thread)");
+    for (size_t s = 0; s < ns; s++) {
+      if (hipMemcpyAsync(d_words + wa[s], words + W0 + wa[s], (wb[s] - wa[s]) * 8, hipMemcpyHostToDevice,
+                         c->side[0]) != hipSuccess ||
+          hipEventRecord(ev_in.ev[s], c->side[0]) != hipSuccess)
+        return ps.fail_with("stream upload failed");
+      ps.post(0, s + 1);
+    }
+  });
+  std::thread down([&] {
+    if (hipSetDevice(c->device) != hipSuccess)
+      return ps.fail_with("hipSetDevice failed (download thread)");
+    for (size_t s = 0; s < ns; s++) {
+      if (!ps.wait(1, s + 1))
+        return;
+      if (hipStreamWaitEvent(c->side[1], ev_k.ev[s], 0) != hipSuccess ||
+          !copy_box(c, sl[s].p, field_base, d_img, es, true, c->side[1]))
+        return ps.fail_with("field download failed");
+    }
+    if (hipStreamSynchronize(c->side[1]) != hipSuccess)
+      ps.fail_with("field download failed");
+  });
+  int ok = 1;
+  for (size_t s = 0; s < ns && ok; s++) {
+    if (!ps.wait(0, s + 1)) {
+      ok = 0;
+      break;
+    }
+    if (hipStreamWaitEvent(c->stream, ev_in.ev[s], 0) != hipSuccess) {
+      ok = fail("hipStreamWaitEvent failed");
+      break;
+    }
+    const uint64_t o = bit_offset + sl[s].b0 * mb;
+    ok = launch_decode<S>(c, sl[s].p, (S*)d_img, d_words + wa[s], wb[s] - wa[s], (uint32_t)(o & 63), nullptr);
+    if (!ok)
+      break;
+    if (hipEventRecord(ev_k.ev[s], c->stream) != hipSuccess) {
+      ok = fail("hipEventRecord failed");
+      break;
+    }
+    ps.post(1, s + 1);
+  }
+  if (!ok)
+    ps.fail_with(g_err.c_str());
+  up.join();
+  down.join();
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipStreamSynchronize(c->side[0]);
+  if (!ok)
+    return 0;
+  if (ps.failed)
+    return fail("zfp_hip_decompress: %s", ps.err.c_str());
+  *end_bit = bit_offset + p.g.nblocks * mb;
+  return 1;
+}
+
+// ---------------------------------------------------------------------------
 extern "C" {
 
 int zfp_hip_device_count(void)
@@ -861,6 +1205,20 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
   if (p.fixed && W0 + (worst_bits + 63) / 64 > capacity_words)
     return fail("zfp_hip_compress: stream capacity %llu words < %llu needed", (unsigned long long)capacity_words,
                 (unsigned long long)(W0 + (worst_bits + 63) / 64));
+  if (!dev_field && !dev_stream && !getenv("ZFP_HIP_NO_PIPE")) {
+    std::vector<Slab> sl;
+    if (make_slabs(job, field_base, p, p.fixed ? 1 : (p.dims == 4 ? kBlocks4PerWave : 64u), sl)) {
+      const auto t0 = std::chrono::steady_clock::now();
+      const int ok = p.dbl ? compress_slabs<double>(c, p, sl, field_base, words, capacity_words, bit_offset,
+                                                    head_word, index, end_bit)
+                           : compress_slabs<float>(c, p, sl, field_base, words, capacity_words, bit_offset,
+                                                   head_word, index, end_bit);
+      t_timing.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      t_timing.kernel_ms = 0;
+      t_timing.timed = ok != 0;
+      return ok;
+    }
+  }
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   // field
   const void* d_field = field_base;
@@ -884,8 +1242,10 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
     d_out = (uint64_t*)c->words.p;
   }
   uint64_t total = 0;
-  int ok = p.dbl ? launch_encode<double>(c, p, (const double*)d_field, d_out, g0, head_word, index, &total)
-                 : launch_encode<float>(c, p, (const float*)d_field, d_out, g0, head_word, index, &total);
+  Head head;
+  head.val = head_word;
+  int ok = p.dbl ? launch_encode<double>(c, p, (const double*)d_field, d_out, g0, head, index, &total)
+                 : launch_encode<float>(c, p, (const float*)d_field, d_out, g0, head, index, &total);
   if (!ok)
     return 0;
   const uint64_t end = bit_offset + total;
@@ -943,6 +1303,18 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
   nwords = std::min<uint64_t>(nwords, avail);
   const bool dev_field = is_device_ptr(field_base);
   const bool dev_stream = is_device_ptr(words);
+  if (p.fixed && !dev_field && !dev_stream && !getenv("ZFP_HIP_NO_PIPE")) {
+    std::vector<Slab> sl;
+    if (make_slabs(job, field_base, p, 1, sl)) {
+      const auto t0 = std::chrono::steady_clock::now();
+      const int ok = p.dbl ? decompress_slabs<double>(c, p, sl, field_base, words, capacity_words, bit_offset, end_bit)
+                           : decompress_slabs<float>(c, p, sl, field_base, words, capacity_words, bit_offset, end_bit);
+      t_timing.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+      t_timing.kernel_ms = 0;
+      t_timing.timed = ok != 0;
+      return ok;
+    }
+  }
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
   const uint64_t* d_in = words + W0;
   if (!dev_stream) {

@@ -57,7 +57,7 @@ def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=("c2", "c4"), default="c2")
     ap.add_argument("--n", type=int, default=N, help="c2: edge of the per-GPU cube (default 1024)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")

@@ -11,7 +11,7 @@ using namespace zfp_amd;
 
 // reference: encode.c:92-132 with a 64-bit LSB-first writer
 static uint32_t ref_code(std::vector<uint64_t>& w, uint32_t pos0, uint32_t maxbits, uint32_t maxprec,
-                         const uint64_t* planes, int prec)
+                         const uint64_t* planes, int prec, uint32_t size = 64)
 {
   uint32_t kmin = (uint32_t)prec > maxprec ? prec - maxprec : 0;
   uint32_t bits = maxbits, n = 0, pos = pos0;
@@ -22,10 +22,10 @@ static uint32_t ref_code(std::vector<uint64_t>& w, uint32_t pos0, uint32_t maxbi
     bits -= m;
     for (uint32_t i = 0; i < m; i++) put((x >> i) & 1);
     x = m < 64 ? x >> m : 0;
-    for (; bits && n < 64; x >>= 1, n++) {
+    for (; bits && n < size; x >>= 1, n++) {
       bits--;
       if (put(x != 0)) {
-        for (; bits && n < 63; x >>= 1, n++) {
+        for (; bits && n < size - 1; x >>= 1, n++) {
           bits--;
           if (put(x & 1u)) break;
         }
@@ -36,7 +36,7 @@ static uint32_t ref_code(std::vector<uint64_t>& w, uint32_t pos0, uint32_t maxbi
   return pos - pos0;
 }
 
-template <int PREC, bool PLIM>
+template <int PREC, bool PLIM, int SIZE = 64>
 static int run(std::mt19937_64& rng, int trials)
 {
   uint32_t lut[256];
@@ -57,6 +57,8 @@ static int run(std::mt19937_64& rng, int trials)
         default: P[k] = (k > PREC - 4) ? (1ull << (rng() % 64)) : r & (r >> 3); break;
       }
     }
+    for (int k = 0; k < PREC; k++)
+      P[k] &= SIZE == 64 ? ~0ull : (1ull << SIZE) - 1;  // 1D/2D blocks: 4 or 16 coefficients
     uint32_t Pl[PREC], Ph[PREC];
     for (int k = 0; k < PREC; k++) Pl[k] = (uint32_t)P[k], Ph[k] = (uint32_t)(P[k] >> 32);
     const uint32_t pos0 = 1 + (uint32_t)(rng() % 40);
@@ -64,9 +66,9 @@ static int run(std::mt19937_64& rng, int trials)
     for (uint32_t lim_bits : budgets) {
       uint32_t maxprec = (PLIM && t % 3 == 0) ? 1 + (uint32_t)(rng() % PREC) : 64;
       std::vector<uint64_t> rw(200, 0), slot(200, 0);
-      uint32_t rlen = ref_code(rw, pos0, lim_bits, maxprec, P, PREC);
+      uint32_t rlen = ref_code(rw, pos0, lim_bits, maxprec, P, PREC, SIZE);
       OrSlot os{slot.data(), 399};
-      uint32_t end = code_planes<PREC, PLIM>(os, lut, pos0, pos0 + lim_bits, maxprec, Pl, Ph);
+      uint32_t end = code_planes<PREC, PLIM, SIZE>(os, lut, pos0, pos0 + lim_bits, maxprec, Pl, Ph);
       bool ok = end - pos0 == rlen;
       uint32_t e = pos0 + rlen;
       for (uint32_t i = 0; ok && i < (e + 63) / 64; i++) {
@@ -74,11 +76,11 @@ static int run(std::mt19937_64& rng, int trials)
         ok = (slot[i] & m) == (rw[i] & m);
       }
       if (!ok && bad++ < 5)
-        printf("PREC %d PLIM %d trial %d kind %d lim %u maxprec %u: len %u vs ref %u\n", PREC, PLIM, t, kind, lim_bits, maxprec,
+        printf("SIZE %d PREC %d PLIM %d trial %d kind %d lim %u maxprec %u: len %u vs ref %u\n", SIZE, PREC, PLIM, t, kind, lim_bits, maxprec,
                end - pos0, rlen);
     }
   }
-  printf("planes%d plim%d mismatches %d\n", PREC, PLIM, bad);
+  printf("size%d planes%d plim%d mismatches %d\n", SIZE, PREC, PLIM, bad);
   return bad;
 }
 
@@ -89,6 +91,8 @@ int main()
   for (int all : {0, 1}) {  // 1: every wave-level branch entered (other lanes need it)
     emu_any_all = all;
     bad += run<32, true>(rng, 20000) + run<64, true>(rng, 10000) + run<32, false>(rng, 20000) + run<64, false>(rng, 10000);
+    bad += run<32, true, 16>(rng, 10000) + run<64, true, 16>(rng, 5000) + run<32, false, 16>(rng, 10000);
+    bad += run<32, true, 4>(rng, 10000) + run<64, true, 4>(rng, 5000) + run<64, false, 4>(rng, 5000);
   }
   printf("mismatches %d\n", bad);
   return bad != 0;

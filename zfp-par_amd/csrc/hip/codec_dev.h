@@ -50,6 +50,31 @@ struct Traits<double> {
   static constexpr UInt kTcMask = 0x7fffffffffffffffull;
 };
 
+// integer fields (encodei.c / decodei.c, traitsi.h, traitsl.h): no exponent
+template <>
+struct Traits<int32_t> {
+  using Int = int32_t;
+  using UInt = uint32_t;
+  static constexpr int kEbits = 0;
+  static constexpr int kPbits = 5;
+  static constexpr int kEbias = 0;
+  static constexpr int kIntPrec = 32;
+  static constexpr UInt kNbMask = 0xaaaaaaaau;
+  static constexpr UInt kTcMask = 0;
+};
+
+template <>
+struct Traits<int64_t> {
+  using Int = int64_t;
+  using UInt = uint64_t;
+  static constexpr int kEbits = 0;
+  static constexpr int kPbits = 6;
+  static constexpr int kEbias = 0;
+  static constexpr int kIntPrec = 64;
+  static constexpr UInt kNbMask = 0xaaaaaaaaaaaaaaaaull;
+  static constexpr UInt kTcMask = 0;
+};
+
 struct CodecParams {
   uint32_t minbits, maxbits, maxprec;
   int32_t minexp;
@@ -555,7 +580,9 @@ __device__ __forceinline__ uint32_t opaque_shr5(uint32_t x)
 #endif
 }
 
-template <int PREC, bool PLIM>
+// SIZE: coefficients per block (4^d; 64 for 3D).  Only the block's last
+// coefficient (implicit one and test) and the all-significant plane depend on it.
+template <int PREC, bool PLIM, int SIZE = 64>
 __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, uint32_t pos, uint32_t lim,
                                                 uint32_t maxprec, const uint32_t (&Pl)[PREC],
                                                 const uint32_t (&Ph)[PREC])
@@ -587,7 +614,8 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
     const uint32_t n1 = nz ? 64u - clz : n;
     const uint64_t S1 = nz ? (~0ull >> clz) : (((uint64_t)Sh << 32) | Sl);
     const uint32_t t2 = (uint32_t)__popc(Nh) + ((uint32_t)__popc(Nl) + n1);  // n' + c
-    const uint32_t impl = Nh >> 31;                                         // top one is coefficient 63
+    // top one is the last coefficient (SIZE - 1)
+    const uint32_t impl = SIZE == 64 ? Nh >> 31 : (uint32_t)(N >> (SIZE - 1)) & 1u;
     const uint64_t xs = N >> (n & 63u);  // n == 64 only with N == 0
     const uint32_t x0 = (uint32_t)xs;
     const uint32_t b0 = x0 & 0xffu;
@@ -597,8 +625,9 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
     const uint32_t l0 = lut[b0], l1 = lut[(x0 >> 8) & 0xffu];
     const uint32_t m = (2u | impl) << ((t2 + nn) & 31u);  // surplus of the top pair at h + c
     const uint32_t h = n1 + nn;  // top one of xs (when nz)
-    const bool ext = act && nz && h >= 16u;
-    const int32_t dlen = (int32_t)t2 + 1 + ((int32_t)(uint32_t)(S1 >> 32) >> 31) + ((int32_t)Nh >> 31);
+    const bool ext = SIZE > 16 && act && nz && h >= 16u;
+    const int32_t dlen = SIZE == 64 ? (int32_t)t2 + 1 + ((int32_t)(uint32_t)(S1 >> 32) >> 31) + ((int32_t)Nh >> 31)
+                                    : (int32_t)t2 + 1 - (int32_t)((S1 >> (SIZE - 1)) & 1u) - (int32_t)impl;
     if (!PLIM) {
       uint32_t* q = dm1 + opaque_shr5(p31);
       const uint32_t t = 31u - p31;
@@ -693,13 +722,14 @@ __device__ __forceinline__ uint32_t squeeze_entry(uint32_t b)
   return o;
 }
 
+template <int SIZE = 64>
 __device__ __forceinline__ void decode_group_slow(WordReader& r, uint64_t& x, uint32_t& bits, uint32_t& n)
 {
-  while (bits && n < 64) {
+  while (bits && n < (uint32_t)SIZE) {
     bits--;
     if (!r.read1())
       break;
-    uint32_t lim = 63 - n;
+    uint32_t lim = (uint32_t)SIZE - 1 - n;
     if (lim > bits)
       lim = bits;
     uint32_t z = ctz64(r.peek64());
@@ -734,7 +764,7 @@ __device__ __forceinline__ uint32_t squeeze32(const uint32_t* sq, uint32_t f)
 // section is parsed in closed form and its consumption selected); only lanes
 // whose section is not closed-form run the reference loop, in a wave-uniform
 // branch.
-template <bool IMP = true>
+template <bool IMP = true, int SIZE = 64>
 __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
 {
   const uint32_t m = n < bits ? n : bits;
@@ -743,7 +773,7 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   uint64_t x = m ? V & (~0ull >> ((64u - m) & 63u)) : 0ull;
   pos += m;
   uint32_t bl = bits - m;
-  const bool grp = n < 64 && bl != 0;
+  const bool grp = n < (uint32_t)SIZE && bl != 0;
   if (!__any(grp)) {  // every lane's plane is all verbatim (n == 64) or out of budget
     r.pos = pos;
     bits = bl;
@@ -761,12 +791,12 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   const uint64_t mq = (ends - 1) & ~ends;  // bits below q (all when ends == 0)
   const uint32_t ones = (uint32_t)__popcll(S & mq);
   const uint32_t P = q - (ones - 1) / 2;
-  const bool fast = grp && one && ends != 0 && n + P <= 63 && q + 2 <= bl;
+  const bool fast = grp && one && ends != 0 && n + P <= (uint32_t)SIZE - 1 && q + 2 <= bl;
   // The section reaches coefficient 63 before its stop (or runs past the
   // window): the reference parses the k63 = 63 - n tokens below it and sets
   // bit 63 without reading it (decode.c:69-120, n < size - 1).  In the
   // squeezed (token) domain a token costs 1 bit plus 1 if it is a one.
-  const bool imp0 = IMP && grp && one && !fast && (ends == 0 || n + P > 63);
+  const bool imp0 = IMP && grp && one && !fast && (ends == 0 || n + P > (uint32_t)SIZE - 1);
   const uint64_t F = (fast || imp0) ? S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd)) : 0ull;
   const uint32_t Fl = (uint32_t)F, Fh = (uint32_t)(F >> 32);
   uint64_t xx = squeeze32(sq, Fl);
@@ -776,25 +806,25 @@ __device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t
   uint64_t xi = 0;
   bool imp = false;
   if (__any(imp0)) {  // wave-uniform: most planes have no such lane
-    k63 = (63u - n) & 63u;
+    k63 = ((uint32_t)SIZE - 1 - n) & 63u;  // tokens below the last coefficient
     xi = xx & ((1ull << k63) - 1);
     si = k63 + (uint32_t)__popcll(xi);  // section bits of those tokens
     imp = imp0 && si <= 63u && si + 1u <= bl;
   }
   x |= (fast ? xx : (imp ? xi | (1ull << k63) : 0ull)) << (n & 63u);
   const uint32_t used = fast ? q + 2u : (imp ? si + 1u : (grp && !one ? 1u : 0u));
-  n = fast ? n + P : (imp ? 64u : n);
+  n = fast ? n + P : (imp ? (uint32_t)SIZE : n);
   r.pos = pos + used;
   bits = bl - used;
   const bool slow = grp && one && !fast && !imp;
   if (__any(slow)) {
     if (slow)
-      decode_group_slow(r, x, bits, n);
+      decode_group_slow<SIZE>(r, x, bits, n);
   }
   return x;
 }
 
-template <int K, int PREC, bool IMP>
+template <int K, int PREC, bool IMP, int SIZE = 64>
 struct DecodePlanes {
   static __device__ __forceinline__ void run(WordReader& r, const uint32_t* sq, uint64_t (&P)[PREC], uint32_t kmin,
                                              uint32_t& bits, uint32_t& n)
@@ -804,14 +834,14 @@ struct DecodePlanes {
       return;
     // a lane past its precision limit decodes with no budget: no effect
     uint32_t b = act ? bits : 0u;
-    P[K] = decode_plane64<IMP>(r, sq, b, n);
+    P[K] = decode_plane64<IMP, SIZE>(r, sq, b, n);
     bits = act ? b : bits;
-    DecodePlanes<K - 1, PREC, IMP>::run(r, sq, P, kmin, bits, n);
+    DecodePlanes<K - 1, PREC, IMP, SIZE>::run(r, sq, P, kmin, bits, n);
   }
 };
 
-template <int PREC, bool IMP>
-struct DecodePlanes<-1, PREC, IMP> {
+template <int PREC, bool IMP, int SIZE>
+struct DecodePlanes<-1, PREC, IMP, SIZE> {
   static __device__ __forceinline__ void run(WordReader&, const uint32_t*, uint64_t (&)[PREC], uint32_t, uint32_t&,
                                              uint32_t&)
   {
@@ -820,7 +850,7 @@ struct DecodePlanes<-1, PREC, IMP> {
 
 // IMP: closed form for sections reaching coefficient 63 (false for the f64
 // maxprec <= 32 decoder, where it measured slower than the reference loop).
-template <int PREC, bool IMP = true>
+template <int PREC, bool IMP = true, int SIZE = 64>
 __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_t* sq, uint32_t budget,
                                                     uint32_t maxprec, uint64_t (&P)[PREC])
 {
@@ -830,7 +860,7 @@ __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_
 #pragma unroll
   for (int k = 0; k < PREC; k++)
     P[k] = 0;
-  DecodePlanes<PREC - 1, PREC, IMP>::run(r, sq, P, kmin, bits, n);
+  DecodePlanes<PREC - 1, PREC, IMP, SIZE>::run(r, sq, P, kmin, bits, n);
   return budget - bits;
 }
 

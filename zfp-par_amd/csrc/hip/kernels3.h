@@ -15,6 +15,7 @@
 #pragma once
 
 #include "block3.h"
+#include "blockn.h"
 
 namespace zfp_amd {
 
@@ -264,8 +265,10 @@ template <int NB>
 __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
                                           const uint32_t* wrt, uint64_t w, uint64_t start, uint32_t total);
 
-// HI: double with maxprec <= 32 (planes 32..63 only, block3.h encode_ints3)
-template <typename S, bool VEC, bool REV, bool HI = false>
+// HI: double with maxprec <= 32 (planes 32..63 only, block3.h encode_ints3).
+// D: block dimensionality; 1D/2D blocks and integer fields take the generic
+// per-lane codec (blockn.h).
+template <typename S, bool VEC, bool REV, bool HI = false, int D = 3>
 __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        GeneralArgs a)
 {
@@ -296,10 +299,15 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   uint32_t len = 0;
   if (live && b < g.nblocks) {
     S v[64];
-    BlockPos p = block_pos(g, b, 3);
-    gather3<S, VEC>(v, data, g, p);
+    BlockPos p = block_pos(g, b, D);
     OrSlot os{wbase + (size_t)lane * a.swp, 2 * a.swp - 1};
-    len = encode_block3<S, REV, false, HI>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
+    if constexpr (D == 3 && !kIntField<S>) {
+      gather3<S, VEC>(v, data, g, p);
+      len = encode_block3<S, REV, false, HI>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
+    } else {
+      gather_n<S, D>(v, data, g, p);
+      len = encode_block_n<S, D, REV>(os, lut, v, cp);
+    }
   }
   const uint32_t incl = wave_incl_scan(len);
   const uint32_t excl_l = incl - len;
@@ -405,7 +413,7 @@ __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* 
 // stream's pending bits below g0 gets those bits instead), then OR them in.
 // `head_keep` selects bits of the head word's current device value to keep
 // (a host slab pipeline: the bits the previous slab wrote below g0).
-__global__ void fixup_zero(const Partial* __restrict__ partials, uint64_t n, uint64_t* out, uint64_t head_idx,
+static __global__ void fixup_zero(const Partial* __restrict__ partials, uint64_t n, uint64_t* out, uint64_t head_idx,
                            uint64_t head_val, uint64_t head_keep)
 {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -416,7 +424,7 @@ __global__ void fixup_zero(const Partial* __restrict__ partials, uint64_t n, uin
     out[idx] = (idx == head_idx) ? ((out[idx] & head_keep) | head_val) : 0ull;
 }
 
-__global__ void fixup_or(const Partial* __restrict__ partials, uint64_t n, uint64_t* out)
+static __global__ void fixup_or(const Partial* __restrict__ partials, uint64_t n, uint64_t* out)
 {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n)
@@ -444,7 +452,7 @@ struct DecodeArgs {
 // the same offset of their blocks hit different banks), funnel-shifted so the
 // block starts at bit 0.  Staging is cooperative: thread t copies word j of
 // block l for t = l*W + j, so consecutive threads read consecutive stream words.
-template <typename S, bool VEC, bool REV, bool HI = false>
+template <typename S, bool VEC, bool REV, bool HI = false, int D = 3>
 __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
 {
   __shared__ uint32_t sq[256];
@@ -506,9 +514,14 @@ __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g,
   r.w = wslot + (size_t)lane * a.swp;
   r.pos = 0;
   S v[64];
-  decode_block3<S, REV, HI>(r, sq, v, cp);
-  BlockPos p = block_pos(g, b, 3);
-  scatter3<S, VEC>(v, data, g, p);
+  const BlockPos p = block_pos(g, b, D);
+  if constexpr (D == 3 && !kIntField<S>) {
+    decode_block3<S, REV, HI>(r, sq, v, cp);
+    scatter3<S, VEC>(v, data, g, p);
+  } else {
+    decode_block_n<S, D, REV>(r, sq, v, cp);
+    scatter_n<S, D>(v, data, g, p);
+  }
 }
 
 }  // namespace zfp_amd

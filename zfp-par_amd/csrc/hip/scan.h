@@ -33,6 +33,8 @@
 // registers, so global latency is paid once per 512 bits.
 #pragma once
 
+#include <type_traits>
+
 #include "codec_dev.h"
 
 namespace zfp_amd {
@@ -189,6 +191,18 @@ __device__ __forceinline__ uint32_t scan_block(R& rd, uint64_t p, const ScanPara
   using T = Traits<S>;
   constexpr int SIZE = 1 << (2 * DIMS);
   constexpr uint32_t kE = T::kEbits, kP = T::kPbits;
+  if constexpr (std::is_integral<S>::value) {
+    // integer blocks: no header (encode.c:260-280), or the reversible
+    // precision (revencode.c:54-76)
+    uint32_t bits;
+    if constexpr (REV) {
+      const uint32_t prec = (uint32_t)(rd.peek(p) & ((1u << kP) - 1)) + 1;
+      bits = kP + scan_planes<SIZE, T::kIntPrec>(rd, p + kP, sp.maxbits - kP, prec);
+    } else {
+      bits = scan_planes<SIZE, T::kIntPrec>(rd, p, sp.maxbits, sp.maxprec);
+    }
+    return bits < sp.minbits ? sp.minbits : bits;
+  }
   const uint64_t h = rd.peek(p);
   const uint32_t zero_len = sp.minbits > 1 ? sp.minbits : 1u;
   if (!(h & 1))
@@ -264,7 +278,8 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
   rd.ring = ring;
   rd.start(e);
   const bool check = !a.first;
-  const bool runs = a.sp.minbits <= 1;  // a zero block is the single bit "0"
+  // a zero float block is the single bit "0" (integer blocks have no flag)
+  const bool runs = !std::is_integral<S>::value && a.sp.minbits <= 1;
   uint64_t p = e;
   uint64_t wi = lo >> 6;     // bitmap word being assembled
   uint64_t acc = 0;          // this chain's starts in word wi

@@ -26,6 +26,7 @@
 #include <vector>
 
 #include "kernels4.h"
+#include "kernels_n.h"
 #include "scan.h"
 #include "zfp_hip.h"
 
@@ -240,7 +241,9 @@ static bool is_device_ptr(const void* p)
 // job analysis
 struct Plan {
   int dims = 0;
-  bool dbl = false;
+  int type = 0;      // zfp_type: 1 int32, 2 int64, 3 float, 4 double
+  size_t es = 0;     // bytes per value
+  bool dbl = false;  // double (the f64 float kernels)
   Geometry g{};
   CodecParams cp{};
   bool fixed = false;        // every block exactly maxbits bits
@@ -254,12 +257,14 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
 {
   if (!j)
     return fail("null job");
-  if (j->type != 3 && j->type != 4)
-    return fail("zfp_hip: scalar type %d not supported (float and double only)", j->type);
-  if (j->dims != 3 && j->dims != 4)
-    return fail("zfp_hip: %dD fields are not on the MI355X path (3D and 4D only)", j->dims);
+  if (j->type < 1 || j->type > 4)
+    return fail("zfp_hip: scalar type %d not supported", j->type);
+  if (j->dims < 1 || j->dims > 4)
+    return fail("zfp_hip: %dD fields are not supported", j->dims);
   p.dims = j->dims;
+  p.type = j->type;
   p.dbl = j->type == 4;
+  p.es = (j->type == 2 || j->type == 4) ? 8 : 4;
   p.cp.minbits = j->minbits;
   p.cp.maxbits = j->maxbits;
   p.cp.maxprec = j->maxprec;
@@ -295,18 +300,20 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
     return fail("zfp_hip: %llu blocks in one call (at most 2^32 - 1)", (unsigned long long)p.g.nblocks);
   for (int a = 0; a < 3; a++)
     p.g.dv[a] = make_fastdiv(p.g.nb[a]);
-  const int ebits = p.dbl ? 11 : 8, pbits = p.dbl ? 6 : 5, intprec = p.dbl ? 64 : 32;
+  const bool integer = p.type <= 2;
+  const int ebits = integer ? 0 : p.dbl ? 11 : 8, pbits = p.es == 8 ? 6 : 5, intprec = p.es == 8 ? 64 : 32;
   const bool rev = p.cp.minexp < kMinExp;
-  const uint32_t hdr = rev ? 2 + ebits + pbits : 1 + ebits;
-  const uint64_t bvals = p.dims == 4 ? 256 : 64;  // values per block
+  // header bits (zfp.c block bounds): integers have none in lossy modes
+  const uint32_t hdr = integer ? (rev ? pbits : 0) : (rev ? 2 + ebits + pbits : 1 + ebits);
+  const uint64_t bvals = 1ull << (2 * p.dims);  // values per block
   uint64_t body = hdr + (bvals - 1) + bvals * std::min<uint32_t>(p.cp.maxprec, intprec);
   uint64_t bound = body;
   if (p.cp.maxbits >= hdr)
     bound = std::min<uint64_t>(bound, p.cp.maxbits);
   p.bound_bits = (uint32_t)bound;
   p.max_len = std::max<uint32_t>(p.bound_bits, p.cp.minbits);
-  p.fixed = !rev && p.cp.minbits == p.cp.maxbits && p.cp.maxbits >= (uint32_t)(1 + ebits);
-  const size_t es = p.dbl ? 8 : 4;
+  p.fixed = !rev && p.cp.minbits == p.cp.maxbits && p.cp.maxbits >= (uint32_t)(integer ? 1 : 1 + ebits);
+  const size_t es = p.es;
   p.vec = p.g.s[0] == 1 && (p.g.s[1] % 4) == 0 && (p.g.s[2] % 4) == 0 && (p.g.f[0] % 4) == 0 &&
           (p.dims < 4 || (p.g.s[3] % 4) == 0) && ((uintptr_t)field_base % (4 * es)) == 0;
   if (!p.fixed && p.max_len > 0xffff)
@@ -333,42 +340,87 @@ struct Head {
   uint64_t idx_add = 0;
 };
 
+// f(tag) with a null pointer of the field's scalar type
+template <typename F>
+static int by_type(const Plan& p, F&& f)
+{
+  switch (p.type) {
+    case 1: return f((int32_t*)nullptr);
+    case 2: return f((int64_t*)nullptr);
+    case 3: return f((float*)nullptr);
+    default: return f((double*)nullptr);
+  }
+}
+
 static uint64_t head_keep_mask(const Head& h, uint32_t g0) { return h.keep && g0 ? (1ull << g0) - 1 : 0ull; }
 
 // double with maxprec <= 32: the kernels that code planes 32..63 only
 template <typename S>
 static bool hi_planes(const Plan& p)
 {
-  return sizeof(S) == 8 && p.cp.maxprec <= 32;
+  return std::is_same<S, double>::value && p.dims == 3 && p.cp.maxprec <= 32;
+}
+
+// 1D/2D blocks and integer fields: the generic per-lane codec (blockn.h),
+// instantiated in zfp_hip_n32.hip / zfp_hip_n64.hip (separate translation
+// units, compiled in parallel)
+template <typename S, int D>
+static void launch_enc_generic(Ctx* c, const Plan& p, const S* d_field, dim3 grid, dim3 block, size_t lds,
+                               const GeneralArgs& a)
+{
+  launch_encode_n(p.type, D, p.cp.minexp < kMinExp, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
+}
+
+template <typename S, int D>
+static void launch_dec_generic(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 block, size_t lds,
+                               const DecodeArgs& a)
+{
+  launch_decode_n(p.type, D, p.cp.minexp < kMinExp, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
 }
 
 template <typename S, bool HI>
 static void launch_general3(Ctx* c, const Plan& p, const S* d_field, dim3 grid, dim3 block, size_t lds,
                             const GeneralArgs& a)
 {
-  const bool rev = p.cp.minexp < kMinExp;
-  if (p.vec && rev)
-    hipLaunchKernelGGL((encode3_general<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (p.vec)
-    hipLaunchKernelGGL((encode3_general<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (rev)
-    hipLaunchKernelGGL((encode3_general<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else
-    hipLaunchKernelGGL((encode3_general<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  if constexpr (kIntField<S>) {
+    if (p.dims == 1) launch_enc_generic<S, 1>(c, p, d_field, grid, block, lds, a);
+    else if (p.dims == 2) launch_enc_generic<S, 2>(c, p, d_field, grid, block, lds, a);
+    else launch_enc_generic<S, 3>(c, p, d_field, grid, block, lds, a);
+  } else {
+    if (p.dims == 1) return launch_enc_generic<S, 1>(c, p, d_field, grid, block, lds, a);
+    if (p.dims == 2) return launch_enc_generic<S, 2>(c, p, d_field, grid, block, lds, a);
+    const bool rev = p.cp.minexp < kMinExp;
+    if (p.vec && rev)
+      hipLaunchKernelGGL((encode3_general<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else if (p.vec)
+      hipLaunchKernelGGL((encode3_general<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else if (rev)
+      hipLaunchKernelGGL((encode3_general<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else
+      hipLaunchKernelGGL((encode3_general<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  }
 }
 
 template <typename S, bool HI>
 static void launch_decode3(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 block, size_t lds, const DecodeArgs& a)
 {
-  const bool rev = p.cp.minexp < kMinExp;
-  if (p.vec && rev)
-    hipLaunchKernelGGL((decode3<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (p.vec)
-    hipLaunchKernelGGL((decode3<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (rev)
-    hipLaunchKernelGGL((decode3<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else
-    hipLaunchKernelGGL((decode3<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  if constexpr (kIntField<S>) {
+    if (p.dims == 1) launch_dec_generic<S, 1>(c, p, d_field, grid, block, lds, a);
+    else if (p.dims == 2) launch_dec_generic<S, 2>(c, p, d_field, grid, block, lds, a);
+    else launch_dec_generic<S, 3>(c, p, d_field, grid, block, lds, a);
+  } else {
+    if (p.dims == 1) return launch_dec_generic<S, 1>(c, p, d_field, grid, block, lds, a);
+    if (p.dims == 2) return launch_dec_generic<S, 2>(c, p, d_field, grid, block, lds, a);
+    const bool rev = p.cp.minexp < kMinExp;
+    if (p.vec && rev)
+      hipLaunchKernelGGL((decode3<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else if (p.vec)
+      hipLaunchKernelGGL((decode3<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else if (rev)
+      hipLaunchKernelGGL((decode3<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else
+      hipLaunchKernelGGL((decode3<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+  }
 }
 
 // Arguments of the packing encoders (encode3_general, encode4) for `nwaves`
@@ -475,7 +527,12 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
                          const Head& head, zfp_hip_index* index, uint64_t* total_bits)
 {
   if (p.dims == 4)
-    return launch_encode4<S>(c, p, d_field, d_out, g0, head, index, total_bits);
+  {
+    if constexpr (kIntField<S>)
+      return fail("zfp_hip: 4D integer fields are not on the GPU path yet");
+    else
+      return launch_encode4<S>(c, p, d_field, d_out, g0, head, index, total_bits);
+  }
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
   if (ngroups > 0x7fffffffull)
@@ -483,7 +540,8 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   dim3 grid((unsigned)ngroups), block(256);
   // aligned fixed-rate kernel: word-multiple blocks and no precision limit
   // below the integer width (its coder runs every plane until the budget)
-  if (p.fixed && (p.cp.maxbits % 64) == 0 && p.cp.maxprec >= (p.dbl ? 64u : 32u)) {
+  if constexpr (!kIntField<S>)
+  if (p.fixed && (p.cp.maxbits % 64) == 0 && p.cp.maxprec >= (p.dbl ? 64u : 32u) && p.dims == 3) {
     const uint32_t sw = p.cp.maxbits / 64;
     const uint32_t swp = (uint32_t)slot_words_odd(p.cp.maxbits);  // words from sw on are spare
     const uint32_t magic = sw > 1 ? (uint32_t)((0x100000000ull + sw - 1) / sw) : 0u;
@@ -588,7 +646,12 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
                          const zfp_hip_index* index)
 {
   if (p.dims == 4)
-    return launch_decode4<S>(c, p, d_field, d_in, in_words, g0, index);
+  {
+    if constexpr (kIntField<S>)
+      return fail("zfp_hip: 4D integer fields are not on the GPU path yet");
+    else
+      return launch_decode4<S>(c, p, d_field, d_in, in_words, g0, index);
+  }
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   if (!p.fixed && index->nwaves != nwaves)
     return fail("zfp_hip: block index has %llu waves, the 3D layout needs %llu", (unsigned long long)index->nwaves,
@@ -711,26 +774,27 @@ static void launch_scan_pass(Ctx* c, const ScanArgs& a)
   hipLaunchKernelGGL((scan_pass<S, DIMS, REV>), dim3(grid), dim3(256), 0, c->stream, a);
 }
 
-static void launch_scan_dispatch(Ctx* c, const Plan& p, const ScanArgs& a)
+template <typename S>
+static void launch_scan_typed(Ctx* c, const Plan& p, const ScanArgs& a)
 {
   const bool rev = p.cp.minexp < kMinExp;
-  if (p.dbl) {
-    if (p.dims == 4) {
-      if (rev) launch_scan_pass<double, 4, true>(c, a);
-      else launch_scan_pass<double, 4, false>(c, a);
-    } else {
-      if (rev) launch_scan_pass<double, 3, true>(c, a);
-      else launch_scan_pass<double, 3, false>(c, a);
-    }
-  } else {
-    if (p.dims == 4) {
-      if (rev) launch_scan_pass<float, 4, true>(c, a);
-      else launch_scan_pass<float, 4, false>(c, a);
-    } else {
-      if (rev) launch_scan_pass<float, 3, true>(c, a);
-      else launch_scan_pass<float, 3, false>(c, a);
-    }
+  switch (p.dims) {
+    case 1: rev ? launch_scan_pass<S, 1, true>(c, a) : launch_scan_pass<S, 1, false>(c, a); break;
+    case 2: rev ? launch_scan_pass<S, 2, true>(c, a) : launch_scan_pass<S, 2, false>(c, a); break;
+    case 3: rev ? launch_scan_pass<S, 3, true>(c, a) : launch_scan_pass<S, 3, false>(c, a); break;
+    default:
+      if constexpr (!kIntField<S>)
+        rev ? launch_scan_pass<S, 4, true>(c, a) : launch_scan_pass<S, 4, false>(c, a);
+      break;
   }
+}
+
+static void launch_scan_dispatch(Ctx* c, const Plan& p, const ScanArgs& a)
+{
+  by_type(p, [&](auto tag) {
+    launch_scan_typed<std::remove_pointer_t<decltype(tag)>>(c, p, a);
+    return 1;
+  });
 }
 
 static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
@@ -865,7 +929,7 @@ struct Slab {
 static bool make_slabs(const zfp_hip_job* job, const void* field_base, const Plan& p, uint64_t align,
                        std::vector<Slab>& out)
 {
-  const size_t es = p.dbl ? 8 : 4;
+  const size_t es = p.es;
   const uint64_t field_bytes = (uint64_t)(p.span_hi - p.span_lo + 1) * es;
   if (field_bytes < env_mb("ZFP_HIP_PIPE_MIN_MB", 256))
     return false;
@@ -881,7 +945,7 @@ static bool make_slabs(const zfp_hip_job* job, const void* field_base, const Pla
   if (nbo < 2)
     return false;
   const uint64_t layer = p.g.nblocks / nbo;
-  const uint64_t layer_bytes = layer * (p.dims == 4 ? 256u : 64u) * es;
+  const uint64_t layer_bytes = layer * (1ull << (2 * p.dims)) * es;
   uint64_t L = std::max<uint64_t>(1, env_mb("ZFP_HIP_PIPE_SLAB_MB", 128) / layer_bytes);
   if (align > 1) {
     const uint64_t q = align / std::gcd(layer, align);
@@ -1191,7 +1255,7 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
   if (!c)
     return 0;
   t_timing = Timing{};
-  const size_t es = p.dbl ? 8 : 4;
+  const size_t es = p.es;
   const uint64_t W0 = bit_offset >> 6;
   const uint32_t g0 = (uint32_t)(bit_offset & 63);
   if (p.g.nblocks == 0) {
@@ -1209,10 +1273,10 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
     std::vector<Slab> sl;
     if (make_slabs(job, field_base, p, p.fixed ? 1 : (p.dims == 4 ? kBlocks4PerWave : 64u), sl)) {
       const auto t0 = std::chrono::steady_clock::now();
-      const int ok = p.dbl ? compress_slabs<double>(c, p, sl, field_base, words, capacity_words, bit_offset,
-                                                    head_word, index, end_bit)
-                           : compress_slabs<float>(c, p, sl, field_base, words, capacity_words, bit_offset,
-                                                   head_word, index, end_bit);
+      const int ok = by_type(p, [&](auto tag) {
+        using S = std::remove_pointer_t<decltype(tag)>;
+        return compress_slabs<S>(c, p, sl, field_base, words, capacity_words, bit_offset, head_word, index, end_bit);
+      });
       t_timing.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       t_timing.kernel_ms = 0;
       t_timing.timed = ok != 0;
@@ -1244,8 +1308,10 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
   uint64_t total = 0;
   Head head;
   head.val = head_word;
-  int ok = p.dbl ? launch_encode<double>(c, p, (const double*)d_field, d_out, g0, head, index, &total)
-                 : launch_encode<float>(c, p, (const float*)d_field, d_out, g0, head, index, &total);
+  int ok = by_type(p, [&](auto tag) {
+    using S = std::remove_pointer_t<decltype(tag)>;
+    return launch_encode<S>(c, p, (const S*)d_field, d_out, g0, head, index, &total);
+  });
   if (!ok)
     return 0;
   const uint64_t end = bit_offset + total;
@@ -1281,7 +1347,7 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
   if (!c)
     return 0;
   t_timing = Timing{};
-  const size_t es = p.dbl ? 8 : 4;
+  const size_t es = p.es;
   const uint64_t W0 = bit_offset >> 6;
   const uint32_t g0 = (uint32_t)(bit_offset & 63);
   if (p.g.nblocks == 0) {
@@ -1307,8 +1373,10 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
     std::vector<Slab> sl;
     if (make_slabs(job, field_base, p, 1, sl)) {
       const auto t0 = std::chrono::steady_clock::now();
-      const int ok = p.dbl ? decompress_slabs<double>(c, p, sl, field_base, words, capacity_words, bit_offset, end_bit)
-                           : decompress_slabs<float>(c, p, sl, field_base, words, capacity_words, bit_offset, end_bit);
+      const int ok = by_type(p, [&](auto tag) {
+        using S = std::remove_pointer_t<decltype(tag)>;
+        return decompress_slabs<S>(c, p, sl, field_base, words, capacity_words, bit_offset, end_bit);
+      });
       t_timing.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       t_timing.kernel_ms = 0;
       t_timing.timed = ok != 0;
@@ -1339,8 +1407,10 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
     d_img = (char*)c->field.p - p.span_lo * (int64_t)es;
     d_field = d_img;
   }
-  int ok = p.dbl ? launch_decode<double>(c, p, (double*)d_field, d_in, nwords, g0, index)
-                 : launch_decode<float>(c, p, (float*)d_field, d_in, nwords, g0, index);
+  int ok = by_type(p, [&](auto tag) {
+    using S = std::remove_pointer_t<decltype(tag)>;
+    return launch_decode<S>(c, p, (S*)d_field, d_in, nwords, g0, index);
+  });
   if (!ok)
     return 0;
   if (!dev_field && !copy_box(c, p, field_base, d_img, es, true))

@@ -1000,7 +1000,8 @@ static void report(const char* what)
 
 static int variable_rate(const zfp_stream* zfp, const zfp_field* field)
 {
-  uint hdr = (field->type == zfp_type_double) ? 12 : 9;
+  /* integer blocks carry no header in the lossy modes */
+  uint hdr = field->type == zfp_type_double ? 12 : field->type == zfp_type_float ? 9 : 1;
   return !(zfp->minexp >= ZFP_MIN_EXP && zfp->minbits == zfp->maxbits && zfp->maxbits >= hdr);
 }
 

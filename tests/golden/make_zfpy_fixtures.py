@@ -39,6 +39,12 @@ CASES = [
     ("64^3 f64 precision 32 nparts 4", (64, 64, 64), "float64", 4, "precision", 32),
     ("129^3 f32 rate 8 nparts 8", (129, 129, 129), "float32", 8, "rate", 8),
     ("16^4 f32 reversible nparts 4", (16, 16, 16, 16), "float32", 4, "reversible", None),
+    # 1D/2D and integer fields
+    ("96x128 i32 rate 12 nparts 4", (96, 128), "int32", 4, "rate", 12),
+    ("40x72 f64 reversible nparts 2", (40, 72), "float64", 2, "reversible", None),
+    ("4000 f32 precision 14 nparts 2", (4000,), "float32", 2, "precision", 14),
+    ("24^3 i64 precision 40 nparts 2", (24, 24, 24), "int64", 2, "precision", 40),
+    ("12^4 i32 reversible nparts 2", (12, 12, 12, 12), "int32", 2, "reversible", None),
 ]
 
 
@@ -46,8 +52,11 @@ def case_field(shape, dtype, seed=2024):
     """Deterministic input: a smooth part on a 1/64 grid plus seeded integer noise / 256."""
     rng = np.random.default_rng(seed)
     g = np.indices(shape, dtype=np.int64)
-    smooth = (g[-1] * 3 + g[-2] * 5 - g[0] * 2) % 97 - 48  # integers
+    y = g[-2] if len(shape) > 1 else 0
+    smooth = (g[-1] * 3 + y * 5 - g[0] * 2) % 97 - 48  # integers
     noise = rng.integers(-128, 128, size=shape)
+    if np.dtype(dtype).kind == "i":  # integer fields: the same pattern, scaled
+        return (smooth * 4096 + noise).astype(dtype)
     return (smooth.astype(np.float64) / 64.0 + noise.astype(np.float64) / 256.0).astype(dtype)
 
 

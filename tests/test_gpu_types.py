@@ -1,7 +1,8 @@
-"""1D/2D fields of every scalar type and 3D integer fields on the GPU.
+"""1D/2D fields of every scalar type and 3D/4D integer fields on the GPU.
 
 The generic per-lane codec (blockn.h: encode_block_n / decode_block_n, the
-closed-form coder with 4^d coefficients) against the reference library itself
+closed-form coder with 4^d coefficients) and the integer branch of the 4D quad
+codec (block4.h) against the reference library itself
 (oracle/_ref, compiled from /root/reference): compressed bytes and
 decompressed arrays identical, through the C API exactly as the reference's
 end-to-end tests call it (tests/src/endtoend/zfpEndtoendBase.c).
@@ -43,7 +44,7 @@ CASES = []
 for dtype in (np.float32, np.float64, np.int32, np.int64):
     shapes = [(1000,), (37,), (45, 67), (64, 64)]
     if np.dtype(dtype).kind == "i":
-        shapes += [(20, 24, 28), (9, 13, 7)]
+        shapes += [(20, 24, 28), (9, 13, 7), (12, 9, 10, 11), (8, 16, 16, 16)]
     for shape in shapes:
         for mode, param in _modes(dtype):
             CASES.append((np.dtype(dtype).name, shape, mode, param))

@@ -55,6 +55,9 @@ def test_oracle_and_header_writer_reproduce_reference_chunks(case, oracle):
     import zfpy
     from zfpy import zfpy_c
     shape, dtype = tuple(case["shape"]), np.dtype(case["dtype"])
+    if len(shape) < 3 or dtype.kind == "i":
+        pytest.skip("the oracle restates the 3D/4D float codec; 1D/2D/integer parity is checked against "
+                    "oracle/_ref in test_gpu_types.py and against these fixtures on the GPU")
     arr = case_field(shape, dtype)
     ck = zfpy_c.zfp_chunkit(arr, np.prod([(n + 3) // 4 for n in shape]) / case["nparts"])
     assert ck.get_nchunks() == case["nchunks"]

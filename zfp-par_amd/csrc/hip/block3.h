@@ -86,6 +86,12 @@ __device__ __forceinline__ BlockPos block_pos(const Geometry& g, uint64_t b64, i
   return p;
 }
 
+// 16 bytes of scalars, for one vector load/store
+template <typename S, int N>
+struct alignas(16) Vec16 {
+  S v[N];
+};
+
 template <typename S, bool VEC>
 __device__ __forceinline__ void gather3(S (&v)[64], const S* __restrict__ base, const Geometry& g, const BlockPos& p)
 {
@@ -98,19 +104,19 @@ __device__ __forceinline__ void gather3(S (&v)[64], const S* __restrict__ base, 
       for (int j = 0; j < 4; j++) {
         const S* r = o + j * sy + k * sz;
         if (VEC) {
+          // 16-byte loads of any scalar type (4 floats/int32 or 2 doubles/int64)
           if constexpr (sizeof(S) == 4) {
-            float4 q = *reinterpret_cast<const float4*>(r);
-            v[16 * k + 4 * j + 0] = q.x;
-            v[16 * k + 4 * j + 1] = q.y;
-            v[16 * k + 4 * j + 2] = q.z;
-            v[16 * k + 4 * j + 3] = q.w;
+            const Vec16<S, 4> q = *reinterpret_cast<const Vec16<S, 4>*>(r);
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              v[16 * k + 4 * j + i] = q.v[i];
           } else {
-            double2 q0 = *reinterpret_cast<const double2*>(r);
-            double2 q1 = *reinterpret_cast<const double2*>(r + 2);
-            v[16 * k + 4 * j + 0] = q0.x;
-            v[16 * k + 4 * j + 1] = q0.y;
-            v[16 * k + 4 * j + 2] = q1.x;
-            v[16 * k + 4 * j + 3] = q1.y;
+            const Vec16<S, 2> q0 = *reinterpret_cast<const Vec16<S, 2>*>(r);
+            const Vec16<S, 2> q1 = *reinterpret_cast<const Vec16<S, 2>*>(r + 2);
+            v[16 * k + 4 * j + 0] = q0.v[0];
+            v[16 * k + 4 * j + 1] = q0.v[1];
+            v[16 * k + 4 * j + 2] = q1.v[0];
+            v[16 * k + 4 * j + 3] = q1.v[1];
           }
         } else {
 #pragma unroll
@@ -158,12 +164,19 @@ __device__ __forceinline__ void scatter3(const S (&v)[64], S* __restrict__ base,
         S* r = o + j * sy + k * sz;
         if (VEC) {
           if constexpr (sizeof(S) == 4) {
-            float4 q = make_float4(v[16 * k + 4 * j + 0], v[16 * k + 4 * j + 1], v[16 * k + 4 * j + 2],
-                                   v[16 * k + 4 * j + 3]);
-            *reinterpret_cast<float4*>(r) = q;
+            Vec16<S, 4> q;
+#pragma unroll
+            for (int i = 0; i < 4; i++)
+              q.v[i] = v[16 * k + 4 * j + i];
+            *reinterpret_cast<Vec16<S, 4>*>(r) = q;
           } else {
-            *reinterpret_cast<double2*>(r) = make_double2(v[16 * k + 4 * j + 0], v[16 * k + 4 * j + 1]);
-            *reinterpret_cast<double2*>(r + 2) = make_double2(v[16 * k + 4 * j + 2], v[16 * k + 4 * j + 3]);
+            Vec16<S, 2> q0, q1;
+            q0.v[0] = v[16 * k + 4 * j + 0];
+            q0.v[1] = v[16 * k + 4 * j + 1];
+            q1.v[0] = v[16 * k + 4 * j + 2];
+            q1.v[1] = v[16 * k + 4 * j + 3];
+            *reinterpret_cast<Vec16<S, 2>*>(r) = q0;
+            *reinterpret_cast<Vec16<S, 2>*>(r + 2) = q1;
           }
         } else {
 #pragma unroll

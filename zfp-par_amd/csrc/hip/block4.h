@@ -20,6 +20,8 @@
 //                212-246, inverse transform decode4.c:27-52.
 #pragma once
 
+#include <type_traits>
+
 #include "block3.h"
 
 namespace zfp_amd {
@@ -416,7 +418,38 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
   OrSlot os{reinterpret_cast<uint64_t*>(d), jmax};
   Int q[64];
   uint32_t Pl[PREC], Ph[PREC];
-  if constexpr (REV) {
+  if constexpr (std::is_integral<S>::value) {
+    // integer blocks (encode.c:260-280, revencode.c:54-76): no exponent, and
+    // only the reversible mode has a header (the precision)
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      q[i] = (Int)v[i];
+    xform<3, false, REV>(q);
+    exchange_fwd<REV>(q, X, tab);
+    zero_region(region, region_words);
+    uint32_t prec = cp.maxprec, bits = 0;
+    if constexpr (REV) {
+      UInt all = 0;
+#pragma unroll
+      for (int i = 0; i < 64; i++)
+        all |= ((UInt)q[i] + T::kNbMask) ^ T::kNbMask;
+      all = quad_or(all);
+      prec = all ? (uint32_t)(PREC - (sizeof(S) == 4 ? __builtin_ctz((uint32_t)all) : __builtin_ctzll((uint64_t)all)))
+                 : 0u;
+      if (prec > cp.maxprec) prec = cp.maxprec;
+      if (prec < 1) prec = 1;
+      if (r == 0u) os.head(prec - 1);
+      bits = T::kPbits;
+    }
+    if constexpr (PREC == 32)
+      planes_from_coeffs<false>(Pl, Ph, q);
+    else
+      planes_from_coeffs<false>(Pl, Ph, q, prec > 32);
+    pin_registers(Pl);
+    pin_registers(Ph);
+    const uint32_t end = code_planes4<PREC>(d, jmax, lut, bits, cp.maxbits, prec, Pl, Ph);
+    return end < cp.minbits ? cp.minbits : end;
+  } else if constexpr (REV) {
     // reversible (revencodef.c:45-80)
     const int emax = block_emax(quad_absmax(v));
     bool same = true;
@@ -524,50 +557,74 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
     q[i] = 0;
   int emax = 0;
   uint32_t kind = 0;  // 0: zero block, 1: block-floating-point, 2: reinterpreted bits
-  if (valid && rd.read1()) {
-    uint32_t bits = 1;
-    uint32_t prec;
-    if constexpr (REV) {
-      bits++;
-      const bool reinterp = rd.read1() != 0;
-      if (!reinterp) {
-        bits += kE;
-        emax = (int)rd.read(kE) - T::kEbias;
+  if constexpr (std::is_integral<S>::value) {
+    // integer blocks (decode.c:271-287, revdecode.c:34-52)
+    if (valid) {
+      uint32_t prec = cp.maxprec, bits = 0;
+      if constexpr (REV) {
+        prec = (uint32_t)rd.read(T::kPbits) + 1;
+        bits = T::kPbits;
       }
-      prec = (uint32_t)rd.read(T::kPbits) + 1;
-      bits += T::kPbits;
-      kind = reinterp ? 2u : (emax != -T::kEbias ? 1u : 0u);
-    } else {
-      bits += kE;
-      emax = (int)rd.read(kE) - T::kEbias;
-      prec = precision4(emax, cp);
-      kind = 1;
-    }
-    uint64_t P[PREC];
-    decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
-    pin_registers(P);
-    if constexpr (PREC == 32)
-      coeffs_from_planes<false>(q, P);
-    else
-      coeffs_from_planes<false>(q, P, prec > 32);
-  }
-  exchange_inv<REV>(q, X, tab);
-  xform<3, true, REV>(q);
-  if (REV && kind == 2u) {
-#pragma unroll
-    for (int i = 0; i < 64; i++) {
-      const Int x = q[i] < 0 ? (Int)((UInt)q[i] ^ T::kTcMask) : q[i];
-      if constexpr (sizeof(S) == 4)
-        v[i] = __uint_as_float((uint32_t)x);
+      uint64_t P[PREC];
+      decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+      pin_registers(P);
+      if constexpr (PREC == 32)
+        coeffs_from_planes<false>(q, P);
       else
-        v[i] = __longlong_as_double((long long)x);
+        coeffs_from_planes<false>(q, P, prec > 32);
     }
-  } else if (kind == 1u) {
-    inv_cast(v, q, emax);
-  } else {
+    exchange_inv<REV>(q, X, tab);
+    xform<3, true, REV>(q);
 #pragma unroll
     for (int i = 0; i < 64; i++)
-      v[i] = 0;
+      v[i] = (S)q[i];
+    return;
+  } else {
+    if (valid && rd.read1()) {
+      uint32_t bits = 1;
+      uint32_t prec;
+      if constexpr (REV) {
+        bits++;
+        const bool reinterp = rd.read1() != 0;
+        if (!reinterp) {
+          bits += kE;
+          emax = (int)rd.read(kE) - T::kEbias;
+        }
+        prec = (uint32_t)rd.read(T::kPbits) + 1;
+        bits += T::kPbits;
+        kind = reinterp ? 2u : (emax != -T::kEbias ? 1u : 0u);
+      } else {
+        bits += kE;
+        emax = (int)rd.read(kE) - T::kEbias;
+        prec = precision4(emax, cp);
+        kind = 1;
+      }
+      uint64_t P[PREC];
+      decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+      pin_registers(P);
+      if constexpr (PREC == 32)
+        coeffs_from_planes<false>(q, P);
+      else
+        coeffs_from_planes<false>(q, P, prec > 32);
+    }
+    exchange_inv<REV>(q, X, tab);
+    xform<3, true, REV>(q);
+    if (REV && kind == 2u) {
+#pragma unroll
+      for (int i = 0; i < 64; i++) {
+        const Int x = q[i] < 0 ? (Int)((UInt)q[i] ^ T::kTcMask) : q[i];
+        if constexpr (sizeof(S) == 4)
+          v[i] = __uint_as_float((uint32_t)x);
+        else
+          v[i] = __longlong_as_double((long long)x);
+      }
+    } else if (kind == 1u) {
+      inv_cast(v, q, emax);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 64; i++)
+        v[i] = 0;
+    }
   }
 }
 

@@ -5,6 +5,7 @@
 #pragma once
 
 #include "kernels3.h"
+#include "kernels4.h"
 
 namespace zfp_amd {
 
@@ -22,6 +23,17 @@ void launch_encode_n64(int type, int dims, bool rev, hipStream_t stream, dim3 gr
                        const void* field, const Geometry& g, const CodecParams& cp, const GeneralArgs& a);
 void launch_decode_n64(int type, int dims, bool rev, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
                        void* field, const Geometry& g, const CodecParams& cp, const DecodeArgs& a);
+
+// 4D integer fields (encode4 / decode4 with an integer scalar)
+void launch_encode4_int(int type, bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
+                        const void* field, const Geometry& g, const CodecParams& cp, const GeneralArgs& a);
+void launch_decode4_int(int type, bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
+                        void* field, const Geometry& g, const CodecParams& cp, const DecodeArgs& a);
+
+void launch_encode4_int64(bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
+                          const void* field, const Geometry& g, const CodecParams& cp, const GeneralArgs& a);
+void launch_decode4_int64(bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds, void* field,
+                          const Geometry& g, const CodecParams& cp, const DecodeArgs& a);
 
 inline void launch_encode_n(int type, int dims, bool rev, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
                             const void* field, const Geometry& g, const CodecParams& cp, const GeneralArgs& a)
@@ -62,6 +74,24 @@ struct GenericKernels {
       hipLaunchKernelGGL((decode3<S, false, true, false, D>), grid, block, lds, st, (S*)f, g, cp, a);
     else
       hipLaunchKernelGGL((decode3<S, false, false, false, D>), grid, block, lds, st, (S*)f, g, cp, a);
+  }
+  static void encode4i(bool rev, bool vec, hipStream_t st, dim3 grid, dim3 block, size_t lds, const void* f,
+                       const Geometry& g, const CodecParams& cp, const GeneralArgs& a)
+  {
+    const A* d = (const A*)f;
+    if (vec && rev) hipLaunchKernelGGL((encode4<A, true, true>), grid, block, lds, st, d, g, cp, a);
+    else if (vec) hipLaunchKernelGGL((encode4<A, true, false>), grid, block, lds, st, d, g, cp, a);
+    else if (rev) hipLaunchKernelGGL((encode4<A, false, true>), grid, block, lds, st, d, g, cp, a);
+    else hipLaunchKernelGGL((encode4<A, false, false>), grid, block, lds, st, d, g, cp, a);
+  }
+  static void decode4i(bool rev, bool vec, hipStream_t st, dim3 grid, dim3 block, size_t lds, void* f,
+                       const Geometry& g, const CodecParams& cp, const DecodeArgs& a)
+  {
+    A* d = (A*)f;
+    if (vec && rev) hipLaunchKernelGGL((decode4<A, true, true>), grid, block, lds, st, d, g, cp, a);
+    else if (vec) hipLaunchKernelGGL((decode4<A, true, false>), grid, block, lds, st, d, g, cp, a);
+    else if (rev) hipLaunchKernelGGL((decode4<A, false, true>), grid, block, lds, st, d, g, cp, a);
+    else hipLaunchKernelGGL((decode4<A, false, false>), grid, block, lds, st, d, g, cp, a);
   }
   static void encode(int type, int dims, bool rev, hipStream_t st, dim3 grid, dim3 block, size_t lds, const void* f,
                      const Geometry& g, const CodecParams& cp, const GeneralArgs& a)

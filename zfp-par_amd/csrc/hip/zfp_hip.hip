@@ -509,7 +509,9 @@ static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_o
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   dim3 grid((unsigned)nwaves), block(64);
   const bool rev = p.cp.minexp < kMinExp;
-  if (p.vec && rev)
+  if constexpr (kIntField<S>)
+    launch_encode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
+  else if (p.vec && rev)
     hipLaunchKernelGGL((encode4<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   else if (p.vec)
     hipLaunchKernelGGL((encode4<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
@@ -527,12 +529,7 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
                          const Head& head, zfp_hip_index* index, uint64_t* total_bits)
 {
   if (p.dims == 4)
-  {
-    if constexpr (kIntField<S>)
-      return fail("zfp_hip: 4D integer fields are not on the GPU path yet");
-    else
-      return launch_encode4<S>(c, p, d_field, d_out, g0, head, index, total_bits);
-  }
+    return launch_encode4<S>(c, p, d_field, d_out, g0, head, index, total_bits);
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
   if (ngroups > 0x7fffffffull)
@@ -628,7 +625,9 @@ static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_i
   dim3 grid((unsigned)nwaves), block(64);
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   const bool rev = p.cp.minexp < kMinExp;
-  if (p.vec && rev)
+  if constexpr (kIntField<S>)
+    launch_decode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
+  else if (p.vec && rev)
     hipLaunchKernelGGL((decode4<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   else if (p.vec)
     hipLaunchKernelGGL((decode4<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
@@ -646,12 +645,7 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
                          const zfp_hip_index* index)
 {
   if (p.dims == 4)
-  {
-    if constexpr (kIntField<S>)
-      return fail("zfp_hip: 4D integer fields are not on the GPU path yet");
-    else
-      return launch_decode4<S>(c, p, d_field, d_in, in_words, g0, index);
-  }
+    return launch_decode4<S>(c, p, d_field, d_in, in_words, g0, index);
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   if (!p.fixed && index->nwaves != nwaves)
     return fail("zfp_hip: block index has %llu waves, the 3D layout needs %llu", (unsigned long long)index->nwaves,
@@ -782,10 +776,7 @@ static void launch_scan_typed(Ctx* c, const Plan& p, const ScanArgs& a)
     case 1: rev ? launch_scan_pass<S, 1, true>(c, a) : launch_scan_pass<S, 1, false>(c, a); break;
     case 2: rev ? launch_scan_pass<S, 2, true>(c, a) : launch_scan_pass<S, 2, false>(c, a); break;
     case 3: rev ? launch_scan_pass<S, 3, true>(c, a) : launch_scan_pass<S, 3, false>(c, a); break;
-    default:
-      if constexpr (!kIntField<S>)
-        rev ? launch_scan_pass<S, 4, true>(c, a) : launch_scan_pass<S, 4, false>(c, a);
-      break;
+    default: rev ? launch_scan_pass<S, 4, true>(c, a) : launch_scan_pass<S, 4, false>(c, a); break;
   }
 }
 

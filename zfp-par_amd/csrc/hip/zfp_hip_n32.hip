@@ -16,4 +16,22 @@ void launch_decode_n32(int type, int dims, bool rev, hipStream_t stream, dim3 gr
   GenericKernels<int32_t, float>::decode(type, dims, rev, stream, grid, block, lds, field, g, cp, a);
 }
 
+void launch_encode4_int(int type, bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
+                        const void* field, const Geometry& g, const CodecParams& cp, const GeneralArgs& a)
+{
+  if (type == 1)
+    GenericKernels<int32_t, float>::encode4i(rev, vec, stream, grid, block, lds, field, g, cp, a);
+  else
+    launch_encode4_int64(rev, vec, stream, grid, block, lds, field, g, cp, a);
+}
+
+void launch_decode4_int(int type, bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
+                        void* field, const Geometry& g, const CodecParams& cp, const DecodeArgs& a)
+{
+  if (type == 1)
+    GenericKernels<int32_t, float>::decode4i(rev, vec, stream, grid, block, lds, field, g, cp, a);
+  else
+    launch_decode4_int64(rev, vec, stream, grid, block, lds, field, g, cp, a);
+}
+
 }  // namespace zfp_amd

@@ -16,4 +16,16 @@ void launch_decode_n64(int type, int dims, bool rev, hipStream_t stream, dim3 gr
   GenericKernels<int64_t, double>::decode(type, dims, rev, stream, grid, block, lds, field, g, cp, a);
 }
 
+void launch_encode4_int64(bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds,
+                          const void* field, const Geometry& g, const CodecParams& cp, const GeneralArgs& a)
+{
+  GenericKernels<int64_t, double>::encode4i(rev, vec, stream, grid, block, lds, field, g, cp, a);
+}
+
+void launch_decode4_int64(bool rev, bool vec, hipStream_t stream, dim3 grid, dim3 block, size_t lds, void* field,
+                          const Geometry& g, const CodecParams& cp, const DecodeArgs& a)
+{
+  GenericKernels<int64_t, double>::decode4i(rev, vec, stream, grid, block, lds, field, g, cp, a);
+}
+
 }  // namespace zfp_amd

@@ -43,8 +43,8 @@ extern "C" {
 
 /* One (de)compression job: field geometry, chunk box, codec parameters. */
 typedef struct zfp_hip_job {
-  int32_t type;        /* zfp_type: 3 = float, 4 = double */
-  int32_t dims;        /* 3 or 4 (1 and 2: not yet) */
+  int32_t type;        /* zfp_type: 1 = int32, 2 = int64, 3 = float, 4 = double */
+  int32_t dims;        /* 1 .. 4 */
   uint64_t n[4];       /* field extents, x first (zfp_field nx..nw) */
   int64_t s[4];        /* element strides, resolved (zfp_field_stride) */
   uint64_t f[4];       /* chunk box first element per axis (zfp_chunk fx..fw) */

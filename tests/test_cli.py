@@ -116,3 +116,32 @@ def test_cli_header_round_trip_and_stats(cli, product, oracle, tmp_path):
         rr = subprocess.run([REF_CLI, "-f", "-3", "32", "24", "16", "-r", "8", "-h", "-i", str(raw), "-z", str(ref),
                              "-q"], capture_output=True)
         assert rr.returncode == 0 and z.read_bytes() == ref.read_bytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("t,dims,mode", [
+    ("i32", ["-2", "45", "38"], ["-r", "12"]),
+    ("i64", ["-4", "9", "10", "11", "6"], ["-p", "40"]),
+    ("f64", ["-1", "1001"], ["-R"]),
+    ("f32", ["-2", "64", "33"], ["-a", "1e-3"]),
+], ids=["2d-i32-rate", "4d-i64-precision", "1d-f64-reversible", "2d-f32-accuracy"])
+def test_cli_other_instantiations_match_reference_cli(cli, product, tmp_path, t, dims, mode):
+    """1D/2D and integer fields through bin/zfp on the GPU, against the reference's own CLI."""
+    if not os.path.exists(REF_CLI):
+        pytest.skip("reference CLI not built (oracle/_ref)")
+    dtype = {"i32": np.int32, "i64": np.int64, "f32": np.float32, "f64": np.float64}[t]
+    n = int(np.prod([int(x) for x in dims[1:]]))
+    rng = np.random.default_rng(3)
+    x = np.arange(n, dtype=np.float64)
+    vals = 1000 * np.sin(0.01 * x) + rng.standard_normal(n)
+    arr = (vals * (1 << 16)).astype(dtype) if np.dtype(dtype).kind == "i" else vals.astype(dtype)
+    raw = tmp_path / "in.raw"
+    arr.tofile(raw)
+    out, back, ref, rback = (tmp_path / f for f in ("out.zfp", "back.raw", "ref.zfp", "rback.raw"))
+    r = run(["-t", t] + dims + mode + ["-i", str(raw), "-z", str(out), "-o", str(back), "-q"])
+    assert r.returncode == 0, r.stderr
+    rr = subprocess.run([REF_CLI, "-t", t] + dims + mode + ["-i", str(raw), "-z", str(ref), "-o", str(rback), "-q"],
+                        capture_output=True)
+    assert rr.returncode == 0, rr.stderr
+    assert out.read_bytes() == ref.read_bytes()
+    assert back.read_bytes() == rback.read_bytes()

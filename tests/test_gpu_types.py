@@ -83,3 +83,22 @@ def test_header_offset_2d(product, ref_capi, dtype):
         ref_out, _ = ref_capi.decompress(want, a.shape, a.dtype, mode, param, ztype=ztype, header=True)
         out, _ = product.decompress(got, a.shape, a.dtype, mode, param, ztype=ztype, header=True)
         assert out.tobytes() == ref_out.tobytes(), (dtype, mode)
+
+
+@pytest.mark.parametrize("shape,dtype", [((10000,), "float32"), ((90, 70), "float64"), ((50, 60), "int32")])
+def test_threaded_chunks_sharing_pages(product, ref_capi, shape, dtype):
+    """zfp_parallel decompresses the chunks of one array from a thread pool; chunk
+    boundaries in 1D/2D fall inside memory pages, and every byte must still be
+    the reference's (the library copies partial pages to the user array itself)."""
+    import zfpy
+    a = _field(shape, np.dtype(dtype), 9)
+    zp = zfpy.zfp_parallel(shape, dtype, nparts=8)
+    zp.get_numpy_array()[...] = a
+    streams = zp.compress(nthreads=8, precision=20)
+    whole = ref_capi.compress(a, "precision", 20, ztype=TYPES[np.dtype(dtype)])
+    want, _ = ref_capi.decompress(whole, shape, dtype, "precision", 20, ztype=TYPES[np.dtype(dtype)])
+    for _ in range(3):
+        zp.get_numpy_array()[...] = 0
+        zp._compress_data = [bytes(s) for s in streams]
+        zp.decompress(nthreads=8)
+        assert np.ascontiguousarray(zp.get_numpy_array()).tobytes() == want.tobytes()

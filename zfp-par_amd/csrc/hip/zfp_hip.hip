@@ -694,6 +694,39 @@ static void record_timing(Ctx* c)
   }
 }
 
+// Device-to-host copy of `bytes` into user memory that other threads may be
+// filling at the same time (zfpy decompresses the chunks of one array from a
+// thread pool, and chunk boundaries need not fall on pages).  The pageable
+// copy path of the runtime may write whole pages, so only whole pages of the
+// destination are copied directly; the partial pages at either end go through
+// a private buffer and a CPU copy of exactly their bytes.
+static int copy_to_host_exact(void* h, const void* d, size_t bytes, hipStream_t q)
+{
+  constexpr uintptr_t kPage = 4096;
+  const uintptr_t a = (uintptr_t)h, e = a + bytes;
+  const uintptr_t a1 = (a + kPage - 1) & ~(kPage - 1), e1 = e & ~(kPage - 1);
+  if (a1 >= e1) {  // no whole page inside
+    std::vector<char> tmp(bytes);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), d, bytes, hipMemcpyDeviceToHost, q));
+    HIP_TRY(hipStreamSynchronize(q));
+    memcpy(h, tmp.data(), bytes);
+    return 1;
+  }
+  const size_t head = a1 - a, tail = e - e1;
+  HIP_TRY(hipMemcpyAsync((void*)a1, (const char*)d + head, e1 - a1, hipMemcpyDeviceToHost, q));
+  if (head || tail) {
+    std::vector<char> tmp(head + tail);
+    if (head)
+      HIP_TRY(hipMemcpyAsync(tmp.data(), d, head, hipMemcpyDeviceToHost, q));
+    if (tail)
+      HIP_TRY(hipMemcpyAsync(tmp.data() + head, (const char*)d + (e1 - a), tail, hipMemcpyDeviceToHost, q));
+    HIP_TRY(hipStreamSynchronize(q));
+    memcpy(h, tmp.data(), head);
+    memcpy((void*)e1, tmp.data() + head, tail);
+  }
+  return 1;
+}
+
 // copy the box of elements between a host field and a device image of its
 // span (device pointer d_base corresponds to host pointer h_base)
 static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es, bool to_host,
@@ -723,13 +756,30 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
     size_t off = (size_t)p.span_lo * es;
     size_t bytes = (size_t)(p.span_hi - p.span_lo + 1) * es;
     if (to_host)
-      HIP_TRY(hipMemcpyAsync((char*)h_base + off, (char*)d_base + off, bytes, kind, q));
+      return copy_to_host_exact((char*)h_base + off, (char*)d_base + off, bytes, q);
     else
       HIP_TRY(hipMemcpyAsync((char*)d_base + off, (char*)h_base + off, bytes, kind, q));
     return 1;
   }
   if (g.s[0] != 1)
     return fail("zfp_hip: host-resident decompression of a non-slab chunk needs unit x stride");
+  // to host: the span through a private buffer, then exactly the box's rows
+  // (neighbouring boxes of the same array may be written concurrently)
+  if (to_host) {
+    const size_t off0 = (size_t)p.span_lo * es, span = (size_t)(p.span_hi - p.span_lo + 1) * es;
+    std::vector<char> tmp(span);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), (char*)d_base + off0, span, hipMemcpyDeviceToHost, q));
+    HIP_TRY(hipStreamSynchronize(q));
+    const size_t w0 = (size_t)(e[0] - g.f[0]) * es;
+    for (uint64_t w = (p.dims >= 4 ? g.f[3] : 0); w < (p.dims >= 4 ? e[3] : 1); w++)
+      for (uint64_t z = (p.dims >= 3 ? g.f[2] : 0); z < (p.dims >= 3 ? e[2] : 1); z++)
+        for (uint64_t y = (p.dims >= 2 ? g.f[1] : 0); y < (p.dims >= 2 ? e[1] : 1); y++) {
+          const int64_t o = (int64_t)g.f[0] * g.s[0] + (int64_t)y * (p.dims >= 2 ? g.s[1] : 0) +
+                            (int64_t)z * (p.dims >= 3 ? g.s[2] : 0) + (int64_t)w * (p.dims >= 4 ? g.s[3] : 0);
+          memcpy((char*)h_base + o * (int64_t)es, tmp.data() + (o * (int64_t)es - (int64_t)off0), w0);
+        }
+    return 1;
+  }
   // row-wise 2D copies, one per (z, w) slice
   size_t width = (size_t)(e[0] - g.f[0]) * es;
   size_t rows = p.dims >= 2 ? (size_t)(e[1] - g.f[1]) : 1;

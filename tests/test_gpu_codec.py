@@ -171,3 +171,32 @@ def test_fixed_rate_large_field_bit_exact(product, oracle):
     got = product.compress(a, "rate", 16, ztype=3)
     want, end = _oracle_bytes(oracle, a, "rate", 16)
     assert got == want
+
+
+@pytest.mark.parametrize("slot_words,pool", [(3, None), (5, None), (9, None), (5, "7")])
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+@pytest.mark.parametrize("mode,param", [("precision", 32), ("precision", 12), ("accuracy", 1e-3),
+                                        ("reversible", None)])
+def test_short_slots_and_overflow_pool_match_oracle(product, oracle, monkeypatch, slot_words, pool, dtype, mode,
+                                                   param):
+    """Variable-rate 3D encoders with short LDS slots: blocks longer than their
+    slot are coded again into the overflow pool (forced here with tiny slots);
+    a pool that runs out makes the library redo the launch with full slots."""
+    monkeypatch.setenv("ZFP_HIP_SLOT_WORDS", str(slot_words))
+    if pool:
+        monkeypatch.setenv("ZFP_HIP_OVF_POOL", pool)
+    rng = np.random.default_rng(zlib.crc32(repr((slot_words, mode, param, np.dtype(dtype).name)).encode()))
+    a = _special_field((40, 36, 33), dtype, rng)
+    a[20:, :, :] = np.sin(np.arange(20 * 36 * 33, dtype=dtype) * 1e-3).reshape(20, 36, 33)  # short blocks too
+    ztype = TYPE_FLOAT if dtype == np.float32 else TYPE_DOUBLE
+    want, end = _oracle_bytes(oracle, a, mode, param)
+    got = product.compress(a, mode, param, ztype=ztype)
+    assert got == want
+    params = _params(mode, param, ztype, a.ndim)
+    ref_out, _ = oracle.decompress_words(np.frombuffer(want, dtype=np.uint64), a.shape, dtype, params)
+    out, n = product.decompress(got, a.shape, dtype, mode, param, ztype=ztype, index=product.last_index)
+    assert n == len(got)
+    assert out.tobytes() == ref_out.tobytes()
+    if product.last_index:
+        product.lib.zfp_hip_index_free(product.last_index)
+        product.last_index = None

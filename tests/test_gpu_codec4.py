@@ -119,3 +119,27 @@ def test_reversible_lossless_4d(product, oracle):
     assert n == len(got)
     assert out.tobytes() == a.tobytes()
     _free_index(product)
+
+
+@pytest.mark.parametrize("slot_words,pool", [(9, None), (21, None), (9, "3")])
+@pytest.mark.parametrize("mode,param", [("precision", 20), ("accuracy", 1e-3), ("reversible", None)])
+def test_short_slots_and_patch_pass_match_oracle_4d(product, oracle, monkeypatch, slot_words, pool, mode, param):
+    """Short-slot 4D encoder: blocks longer than their LDS slot are packed
+    truncated, listed, and ORed in whole by encode4_patch (forced here with
+    tiny slots); an exhausted list makes the library redo the launch with
+    full-size slots.  The exchange areas are shared by quad pairs (HALF)."""
+    monkeypatch.setenv("ZFP_HIP_SLOT_WORDS", str(slot_words))
+    if pool:
+        monkeypatch.setenv("ZFP_HIP_OVF_POOL", pool)
+    rng = np.random.default_rng(zlib.crc32(repr((slot_words, mode, param, 4)).encode()))
+    a = _field4((12, 9, 16, 20), np.float32, rng)
+    a[8:] = np.cos(np.arange(4 * 9 * 16 * 20, dtype=np.float32) * 1e-3).reshape(4, 9, 16, 20)  # short blocks too
+    want, end = _oracle_bytes(oracle, a, mode, param)
+    got = product.compress(a, mode, param, ztype=TYPE_FLOAT)
+    assert got == want
+    params = _params(mode, param, TYPE_FLOAT, a.ndim)
+    ref_out, _ = oracle.decompress_words(np.frombuffer(want, dtype=np.uint64), a.shape, np.float32, params)
+    out, n = product.decompress(got, a.shape, np.float32, mode, param, ztype=TYPE_FLOAT, index=product.last_index)
+    assert n == len(got)
+    assert out.tobytes() == ref_out.tobytes()
+    _free_index(product)

@@ -44,7 +44,11 @@ __global__ __launch_bounds__(256) void vk(uint32_t* out, uint32_t iters)
     if (K == 24) asm volatile("v_ashrrev_i32 %0, %1, %0" : "+v"(a##r) : "v"(s));                          \
     if (K == 25) asm volatile("v_or3_b32 %0, %0, %1, %2" : "+v"(a##r) : "v"(b##r), "v"(s));               \
     if (K == 26) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(a##r) : "v"(b##r));                           \
-    if (K == 27) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(a##r) : "v"(b##r), "v"(s));
+    if (K == 27) asm volatile("v_xad_u32 %0, %0, %1, %2" : "+v"(a##r) : "v"(b##r), "v"(s));               \
+    if (K == 28) asm volatile("v_ashrrev_i64 %0, %1, %0" : "+v"(*(uint64_t*)&a##r) : "v"(s));               \
+    if (K == 29) asm volatile("v_add_co_u32 %0, vcc, %0, %1\n v_addc_co_u32 %0, vcc, %0, %1, vcc" : "+v"(a##r) : "v"(b##r) : "vcc"); \
+    if (K == 30) asm volatile("v_lshl_add_u64 %0, %0, 1, %1" : "+v"(*(uint64_t*)&a##r) : "v"(*(uint64_t*)&b##r)); \
+    if (K == 31) asm volatile("v_mov_b64 %0, %1" : "=v"(*(uint64_t*)&a##r) : "v"(*(uint64_t*)&b##r));
     REP8(OP)
     REP8(OP)
 #undef OP
@@ -89,7 +93,7 @@ int main()
   uint32_t* o; CK(hipMalloc(&o, 64 << 20));
   const char* names[] = {"add_u32", "lshlrev_b64", "bfi", "perm", "bcnt", "ffbh", "alignbit", "add3", "cvt_i32_f32",
                          "lshlrev_b32", "mov", "lshl_or", "bfe_u32", "lshl_sdwa", "cndmask", "max3_i32",
-                         "cndmask_sgpr", "cmp+cndmask", "xor", "and", "sub", "min_u32", "cmp_gt", "lshrrev_b64", "ashrrev", "or3", "mul_f32", "xad"};
+                         "cndmask_sgpr", "cmp+cndmask", "xor", "and", "sub", "min_u32", "cmp_gt", "lshrrev_b64", "ashrrev", "or3", "mul_f32", "xad", "ashrrev_i64", "add_co+addc(2)", "lshl_add_u64", "mov_b64"};
   const uint32_t it = 2048;
   for (int waves_per_simd : {4}) {
     dim3 g(256 * waves_per_simd), b(256);  // 4 waves per group -> 1 per SIMD
@@ -98,7 +102,7 @@ int main()
 #define RUN(K) t = time_it([&] { hipLaunchKernelGGL(vk<K>, g, b, 0, 0, o, it); }); \
     printf("w/simd=%d %-12s %.3f ms  %.2f ns/instr/SIMD\n", waves_per_simd, names[K], t, t * 1e6 / instr_per_simd);
     RUN(0) RUN(1) RUN(2) RUN(3) RUN(4) RUN(5) RUN(6) RUN(7) RUN(8) RUN(9) RUN(10) RUN(11) RUN(12) RUN(13) RUN(14) RUN(15)
-    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26) RUN(27)
+    RUN(16) RUN(17) RUN(18) RUN(19) RUN(20) RUN(21) RUN(22) RUN(23) RUN(24) RUN(25) RUN(26) RUN(27) RUN(28) RUN(29) RUN(30) RUN(31)
 #undef RUN
     double lds_per_cu = (double)waves_per_simd * 4 * it * 8;
     t = time_it([&] { hipLaunchKernelGGL(lk<0>, g, b, 0, 0, o, it); });

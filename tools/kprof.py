@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--decode", action="store_true")
     ap.add_argument("--dims", type=int, default=3)
+    ap.add_argument("--sha", action="store_true", help="print a hash of the last stream (variant exactness)")
     ap.add_argument("--host", action="store_true", help="field and stream in host memory (PCIe-inclusive)")
     ap.add_argument("--lib", default=R + "/zfp-par_amd/lib/libzfp.so", help="libzfp.so to load (variant builds)")
     a = ap.parse_args()
@@ -92,6 +93,10 @@ def main():
     gb = (f.nbytes if a.host else f.numel() * f.element_size()) / 1e9
     print(("host->host call " if a.host else "") + "encode %dD %s %s %s: bytes=%d kernel_ms=%s  GB/s=%.1f" % (a.dims, a.dtype, a.mode, a.param, nb,
           " ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
+    if a.sha:
+        import hashlib
+        raw = out_np[:nb].tobytes() if a.host else out[:nb].cpu().numpy().tobytes()
+        print("stream sha256 %s" % hashlib.sha256(raw).hexdigest()[:16])
     if a.decode:
         if a.host:
             import numpy as np

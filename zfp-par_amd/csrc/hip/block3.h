@@ -521,20 +521,26 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
   if constexpr (REV) {
     // reversible (revencodef.c:45-80)
     int emax = block_emax(block_absmax(v));
-    bool same = true;
+    // bitwise accumulation: a short-circuit && becomes 64 nested lane branches
+    decltype(bits_of(v[0])) sdiff = 0;
+    bool same;
     if (emax != -T::kEbias) {
       fwd_cast(q, v, emax);
       S s = (sizeof(S) == 4) ? (S)pow2f(emax - 30) : (S)pow2d(emax - 62);
 #pragma unroll
-      for (int i = 0; i < 64; i++)
-        same = same && (bits_of((S)(s * (S)q[i])) == bits_of(v[i]));
+      for (int i = 0; i < 64; i++) {
+        sdiff |= bits_of((S)(s * (S)q[i])) ^ bits_of(v[i]);
+        if ((i & 3) == 3)
+          pin_value(sdiff);  // accumulated in order (not as a tree of 64 live terms)
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 64; i++) {
         q[i] = 0;
-        same = same && (bits_of(v[i]) == 0);
+        sdiff |= bits_of(v[i]);
       }
     }
+    same = sdiff == 0;
     uint32_t bits;
     if (same) {
       uint32_t e = (uint32_t)(emax + T::kEbias);
@@ -547,8 +553,10 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
     } else {
 #pragma unroll
       for (int i = 0; i < 64; i++) {
-        Int x = (Int)bits_of(v[i]);
+        const Int x = (Int)bits_of(v[i]);
         q[i] = x < 0 ? (Int)((UInt)x ^ T::kTcMask) : x;
+        if ((i & 3) == 3)
+          ZFP_SCHED_FENCE();
       }
       w.head(3u);
       bits = 2;

@@ -132,35 +132,48 @@ __constant__ OrderTab4 kOrderTab4 = make_order_tab4();
 
 // forward: slices (after the x, y, z lifts) -> w-lift (encode4.c:60-64) ->
 // lane r gets the coefficients of coding order 64r .. 64r+63.  Called by the
-// whole wave (one 64-thread workgroup).
-template <bool REV, typename Int>
+// whole wave (one 64-thread workgroup).  HALF: the exchange areas of quads
+// q and q + 8 coincide (X at (q & 7) * kXStride) and the two halves of the
+// wave take turns, halving the LDS the exchange needs.
+template <bool REV, bool HALF = false, typename Int>
 __device__ __forceinline__ void exchange_fwd(Int (&q)[64], Int* X, const uint32_t* tab)
 {
   const uint32_t r = threadIdx.x & 3u;
+  const uint32_t mine_h = (threadIdx.x >> 5) & 1u;
+#pragma unroll 1
+  for (uint32_t h = 0; h < (HALF ? 2u : 1u); h++) {
+    const bool mine = !HALF || mine_h == h;
+    if (mine) {
 #pragma unroll
-  for (int i = 0; i < 64; i++)
-    X[4 * i + r] = q[i];
-  __syncthreads();
+      for (int i = 0; i < 64; i++)
+        X[4 * i + r] = q[i];
+    }
+    __syncthreads();
+    if (mine) {
 #pragma unroll
-  for (int j = 0; j < 16; j++) {
-    Int* e = X + 4 * (16 * r + j);
-    Int a = e[0], b = e[1], c = e[2], d = e[3];
-    if (REV) Lift<Int>::rfwd(a, b, c, d);
-    else Lift<Int>::fwd(a, b, c, d);
-    e[0] = a;
-    e[1] = b;
-    e[2] = c;
-    e[3] = d;
+      for (int j = 0; j < 16; j++) {
+        Int* e = X + 4 * (16 * r + j);
+        Int a = e[0], b = e[1], c = e[2], d = e[3];
+        if (REV) Lift<Int>::rfwd(a, b, c, d);
+        else Lift<Int>::fwd(a, b, c, d);
+        e[0] = a;
+        e[1] = b;
+        e[2] = c;
+        e[3] = d;
+      }
+    }
+    __syncthreads();
+    if (mine) {
+#pragma unroll
+      for (int m = 0; m < 16; m++) {
+        const uint32_t t = tab[16 * r + m];
+#pragma unroll
+        for (int i = 0; i < 4; i++)
+          q[4 * m + i] = X[(t >> (8 * i)) & 0xffu];
+      }
+    }
+    __syncthreads();
   }
-  __syncthreads();
-#pragma unroll
-  for (int m = 0; m < 16; m++) {
-    const uint32_t t = tab[16 * r + m];
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-      q[4 * m + i] = X[(t >> (8 * i)) & 0xffu];
-  }
-  __syncthreads();
 }
 
 // inverse: coefficients in coding order -> inverse w-lift (decode4.c:31-36) ->
@@ -228,6 +241,9 @@ __device__ __forceinline__ uint64_t dbl32(const uint32_t* lut, uint32_t x)
   return (uint64_t)dbl16(lut, lo) | ((uint64_t)dbl16(lut, x >> 16) << (16u + (uint32_t)__popc(lo)));
 }
 
+#ifndef ZFP_CODER4_BRANCHY
+#define ZFP_CODER4_BRANCHY 0
+#endif
 template <int PREC>
 __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, const uint32_t* lut, uint32_t pos,
                                                  uint32_t lim, uint32_t maxprec, const uint32_t (&Pl)[PREC],
@@ -254,6 +270,7 @@ __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, con
     const uint32_t n1 = top1 ? top1 : n;
     const uint32_t impl = top1 == 256u ? 1u : 0u;  // coefficient 255: its one and test are implicit
     const uint32_t dlen = n1 + ctot + 1u - (n1 == 256u ? 1u : 0u) - impl;
+#if ZFP_CODER4_BRANCHY
     if (act) {
       const uint64_t V = P & S;
       if (nr)
@@ -282,6 +299,31 @@ __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, con
           or64_clamped(d, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
       }
     }
+#else
+    // Straight-line for every lane: an inactive lane (or an empty part) ORs
+    // zeros at a clamped address, so no per-lane branch (and no exec-mask
+    // bookkeeping in SGPRs) is needed.
+    {
+      const uint64_t V = act ? P & S : 0ull;
+      or64_clamped(d, jmax, p + base, (uint32_t)V, (uint32_t)(V >> 32));
+      const uint32_t gp = p + n;  // the plane's positive group test
+      lds_or32(d + min(gp >> 5, jmax), (act && top1 && r == 0u) ? 1u << (gp & 31u) : 0u);
+      const uint64_t xs = (act && nr < 64u) ? N >> nr : 0ull;
+      const uint32_t x0 = (uint32_t)xs, x1 = (uint32_t)(xs >> 32);
+      uint64_t E0 = dbl32(lut, x0), E1 = dbl32(lut, x1);
+      const uint32_t L0 = 32u + (uint32_t)__popc(x0);
+      // top one at xs bit h; its pair starts at h + (c - 1) of the expansion
+      const bool top = bl != 0u && base + bl == top1;
+      const uint32_t h = bl - 1u - nr;
+      const uint32_t t = h + c - 1u;
+      const uint64_t m = top ? (uint64_t)(2u | impl) : 0ull;
+      E0 &= ~(h < 32u ? m << (t & 63u) : 0ull);
+      E1 &= ~(h < 32u ? 0ull : m << ((t - L0) & 63u));
+      const uint32_t co = p + 1u + base + nr + cex;
+      or64_clamped(d, jmax, co, (uint32_t)E0, (uint32_t)(E0 >> 32));
+      or64_clamped(d, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
+    }
+#endif
     p = act ? p + dlen : p;
     n = act ? n1 : n;
   }
@@ -404,7 +446,7 @@ __device__ __forceinline__ int lossy_emax_cast4(int64_t (&q)[64], double (&v)[64
 // returns the block length in bits including minbits padding.  Called by the
 // whole wave: the exchange and the slot zeroing are wave-wide (`region`,
 // `region_words`: the wave's slot area, which aliases the exchange areas).
-template <typename S, bool REV, typename Reload>
+template <typename S, bool REV, bool HALF = false, typename Reload>
 __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, const uint32_t* lut, const uint32_t* tab,
                                                   typename Traits<S>::Int* X, uint64_t* region, uint32_t region_words,
                                                   S (&v)[64], const CodecParams& cp, Reload&& reload)
@@ -425,7 +467,7 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
     for (int i = 0; i < 64; i++)
       q[i] = (Int)v[i];
     xform<3, false, REV>(q);
-    exchange_fwd<REV>(q, X, tab);
+    exchange_fwd<REV, HALF>(q, X, tab);
     zero_region(region, region_words);
     uint32_t prec = cp.maxprec, bits = 0;
     if constexpr (REV) {
@@ -452,30 +494,37 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
   } else if constexpr (REV) {
     // reversible (revencodef.c:45-80)
     const int emax = block_emax(quad_absmax(v));
-    bool same = true;
+    // bitwise accumulation: a short-circuit && becomes 64 nested lane branches
+    decltype(bits_of(v[0])) sdiff = 0;
+    bool same;
     if (emax != -T::kEbias) {
       fwd_cast(q, v, emax);
       const S s = (sizeof(S) == 4) ? (S)pow2f(emax - 30) : (S)pow2d(emax - 62);
 #pragma unroll
-      for (int i = 0; i < 64; i++)
-        same = same && (bits_of((S)(s * (S)q[i])) == bits_of(v[i]));
+      for (int i = 0; i < 64; i++) {
+        sdiff |= bits_of((S)(s * (S)q[i])) ^ bits_of(v[i]);
+        if ((i & 3) == 3)
+          pin_value(sdiff);  // accumulated in order (not as a tree of 64 live terms)
+      }
     } else {
 #pragma unroll
       for (int i = 0; i < 64; i++) {
         q[i] = 0;
-        same = same && (bits_of(v[i]) == 0);
+        sdiff |= bits_of(v[i]);
       }
     }
-    same = quad_or(same ? 0u : 1u) == 0u;
+    same = quad_or(sdiff != 0 ? 1u : 0u) == 0u;
     if (!same) {
 #pragma unroll
       for (int i = 0; i < 64; i++) {
         const Int x = (Int)bits_of(v[i]);
         q[i] = x < 0 ? (Int)((UInt)x ^ T::kTcMask) : x;
+        if ((i & 3) == 3)
+          ZFP_SCHED_FENCE();
       }
     }
     xform<3, false, true>(q);
-    exchange_fwd<true>(q, X, tab);
+    exchange_fwd<true, HALF>(q, X, tab);
     zero_region(region, region_words);
     const uint32_t e = (uint32_t)(emax + T::kEbias);
     if (same && !e)
@@ -517,7 +566,7 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
     const int emax = lossy_emax_cast4(q, v, cp, mp, reload);
     const uint32_t e = mp ? (uint32_t)(emax + T::kEbias) : 0u;
     xform<3, false, false>(q);
-    exchange_fwd<false>(q, X, tab);
+    exchange_fwd<false, HALF>(q, X, tab);
     zero_region(region, region_words);
     uint32_t bits = 1;
     if (e) {

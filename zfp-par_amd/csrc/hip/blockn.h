@@ -249,20 +249,23 @@ __device__ __forceinline__ uint32_t encode_block_n(OrSlot& w, const uint32_t* lu
       m = (m < a) ? a : m;
     }
     const int emax = block_emax(m);
-    bool same = true;
+    // bitwise accumulation: a short-circuit && becomes 64 nested lane branches
+    decltype(bits_of(v[0])) sdiff = 0;
+    bool same;
     if (emax != -T::kEbias) {
       fwd_cast(head_n<N>(q), head_n<N>(v), emax);
       const S s = (sizeof(S) == 4) ? (S)pow2f(emax - 30) : (S)pow2d(emax - 62);
 #pragma unroll
       for (int i = 0; i < N; i++)
-        same = same && (bits_of((S)(s * (S)q[i])) == bits_of(v[i]));
+        sdiff |= bits_of((S)(s * (S)q[i])) ^ bits_of(v[i]);
     } else {
 #pragma unroll
       for (int i = 0; i < N; i++) {
         q[i] = 0;
-        same = same && (bits_of(v[i]) == 0);
+        sdiff |= bits_of(v[i]);
       }
     }
+    same = sdiff == 0;
     if (same) {
       const uint32_t e = (uint32_t)(emax + T::kEbias);
       if (!e)

@@ -185,6 +185,21 @@ __device__ __forceinline__ uint32_t dbl16(const uint32_t* lut, uint32_t u)
   return lut[b0] | (lut[b1] << (8u + (uint32_t)__popc(b0)));
 }
 
+// Scheduling fence (no instruction moves across it).
+#ifdef __HIP_DEVICE_COMPILE__
+#define ZFP_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+#define ZFP_SCHED_FENCE() ((void)0)
+#endif
+
+template <typename U>
+__device__ __forceinline__ void pin_value(U& x)
+{
+#ifdef __HIP_DEVICE_COMPILE__
+  asm volatile("" : "+v"(x));
+#endif
+}
+
 // Materialise every element at this point: the IR passes cannot sink the
 // computation of these values into later (branchy) code, e.g. the last
 // transpose steps into the plane coder, which would keep their inputs live.
@@ -656,8 +671,10 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
     const uint32_t g = ((d16 << 1) | (nz ? 1u : 0u)) - (ext ? 0u : m);
     if (PLIM) {
       if (act) {
-        s.put64(p31 - 31u, pl ^ Nl, ph ^ Nh);  // the n verbatim bits
-        s.put32(p31 - 31u + n, g);
+        // clamped: a short slot (encode3_general) may be outrun by a block
+        // that is coded again into an overflow slot
+        s.put64_clamped(p31 - 31u, pl ^ Nl, ph ^ Nh);  // the n verbatim bits
+        s.put32_clamped(p31 - 31u + n, g);
       }
       p31 = act ? p31 + (uint32_t)dlen : p31;
       n = act ? n1 : n;

@@ -54,6 +54,27 @@ __device__ __forceinline__ void encode_prologue(uint32_t* lut, uint64_t* wslot, 
   __syncthreads();
 }
 
+#ifndef ZFP_EARLY_GATHER
+#define ZFP_EARLY_GATHER 1
+#endif
+// Wave-local prologue: the wave writes all 256 table entries itself (the other
+// waves of the group write the same values), so only its own LDS writes must
+// have landed -- no workgroup barrier, and loads issued before it stay in flight.
+__device__ __forceinline__ void encode_prologue_wave(uint32_t* lut, uint64_t* wslot, uint32_t words)
+{
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int i = 0; i < 4; i++)
+    lut[lane + 64 * i] = dbl_entry(lane + 64 * i);
+  uint4* z = reinterpret_cast<uint4*>(wslot);
+  for (uint32_t i = lane; i < words / 2; i += 64)
+    z[i] = make_uint4(0, 0, 0, 0);
+  if ((words & 1) && lane == 0)
+    wslot[words - 1] = 0;
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only (vmcnt/expcnt at max)
+  __builtin_amdgcn_wave_barrier();
+}
+
 // floor(i / d) for i < 2^20, d < 2^12 with m = ceil(2^32 / d) (m = 0 for d = 1)
 __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m ? __umulhi(i, m) : i; }
 
@@ -74,14 +95,27 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   uint64_t* wslot = lds + (size_t)wv * 64 * swp;
-  encode_prologue(lut, wslot, 64 * swp);
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
+#if ZFP_EARLY_GATHER
+  // the block loads are in flight while the wave fills its tables: every wave
+  // writes the whole (identical) table, so no workgroup barrier is needed
+  S v[64];
+  BlockPos p{};
+  if (b < g.nblocks) {
+    p = block_pos(g, b, 3);
+    gather3<S, VEC>(v, data, g, p);
+  }
+  encode_prologue_wave(lut, wslot, 64 * swp);
+  if (b < g.nblocks) {
+#else
+  encode_prologue(lut, wslot, 64 * swp);
   if (b < g.nblocks) {
     S v[64];
     BlockPos p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
+#endif
     OrSlot os{wslot + (size_t)lane * swp, 2 * swp - 1};
     encode_block3<S, REV, true>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
@@ -145,6 +179,17 @@ __device__ __forceinline__ uint64_t slot_bits(const uint64_t* slot, uint32_t pos
   return v & low_mask(cnt);
 }
 
+// slot_bits from an overflow slot: L2 reads (its words were written by other
+// lanes' atomics)
+__device__ __forceinline__ uint64_t slot_bits_l2(uint64_t* slot, uint32_t pos, uint32_t cnt)
+{
+  uint32_t i = pos >> 6, r = pos & 63;
+  uint64_t v = __hip_atomic_load(slot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >> r;
+  if (r && r + cnt > 64)
+    v |= __hip_atomic_load(slot + i + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) << (64 - r);
+  return v & low_mask(cnt);
+}
+
 struct GeneralArgs {
   uint64_t* out;          // stream words, index 0 = word containing bit g0
   uint32_t g0;            // start bit within out[0]
@@ -157,9 +202,39 @@ struct GeneralArgs {
   uint16_t* idx_len;      // per-block bit lengths (variable rate; optional)
   uint64_t* idx_base;     // per-wave start offsets relative to g0 (optional)
   uint64_t* total_bits;   // written by the last wave (variable rate)
-  uint32_t* error;        // look-back timeout flag
+  uint32_t* error;        // bit 0: look-back timeout; bit 1: overflow pool exhausted
   uint64_t idx_add;       // added to the index bases (offset of this launch in its chunk)
+  // Short LDS slots (variable rate): a slot of swp words holds cap_bits intact
+  // bits; a block that codes longer is coded again into a full-size slot
+  // (ovf_swp words) of the overflow pool in global memory.  ovf == nullptr:
+  // the LDS slots are full size.
+  uint64_t* ovf;
+  uint32_t* ovf_count;    // pool slots handed out (zeroed per launch)
+  uint32_t ovf_cap;       // pool slots
+  uint32_t ovf_swp;       // words per pool slot
+  uint32_t cap_bits;      // intact bits of an LDS slot
 };
+
+// Overflow slot of a lane whose block did not fit its LDS slot: ~0u when none
+// (or when the pool is exhausted: the error flag makes the host redo the
+// launch with full-size slots).
+constexpr uint32_t kNoSlot = ~0u;
+
+__device__ __forceinline__ uint32_t take_overflow_slot(const GeneralArgs& a)
+{
+  uint32_t oi = atomicAdd(a.ovf_count, 1u);
+  if (oi >= a.ovf_cap) {
+    atomicOr(a.error, 2u);
+    oi = kNoSlot;
+  }
+  return oi;
+}
+
+__device__ __forceinline__ void zero_words(uint64_t* p, uint32_t n)
+{
+  for (uint32_t i = 0; i < n; i++)
+    p[i] = 0;
+}
 
 constexpr uint64_t kStAgg = 1ull << 62;
 constexpr uint64_t kStIncl = 2ull << 62;
@@ -261,25 +336,37 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint64_t w, 
   return excl;
 }
 
-template <int NB>
+template <int NB, bool OVF>
 __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
-                                          const uint32_t* wrt, uint64_t w, uint64_t start, uint32_t total);
+                                          const uint32_t* wrt, const uint32_t* ovi, uint64_t w, uint64_t start,
+                                          uint32_t total);
+
+// Waves per SIMD the general encoder is compiled for: the f64 kernels that code
+// planes 32..63 fit three (<= 168 VGPRs) when their LDS slots are short
+// (launch_encode); the others are not bounded.
+template <typename S, bool REV, bool HI>
+constexpr int kGenWaves = (sizeof(S) == 8 && HI) ? 3 : 1;
+
+// Per-wave LDS of encode3_general: 64 slots of swp words, then 64 offsets, 64
+// written counts and 64 overflow slot numbers (uint32).
+__host__ __device__ constexpr uint32_t gen_wave_words(uint32_t swp) { return 64 * swp + 96; }
 
 // HI: double with maxprec <= 32 (planes 32..63 only, block3.h encode_ints3).
 // D: block dimensionality; 1D/2D blocks and integer fields take the generic
 // per-lane codec (blockn.h).
 template <typename S, bool VEC, bool REV, bool HI = false, int D = 3>
-__global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ data, Geometry g, CodecParams cp,
-                                                       GeneralArgs a)
+__global__ __launch_bounds__(256, (kGenWaves<S, REV, HI>)) void encode3_general(const S* __restrict__ data,
+                                                                               Geometry g, CodecParams cp,
+                                                                               GeneralArgs a)
 {
   __shared__ uint32_t lut[256];
   extern __shared__ uint64_t lds[];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  // per wave: 64 slots, then 64 offsets + 64 written counts (uint32)
-  uint64_t* wbase = lds + (size_t)wv * (64 * a.swp + 64);
+  uint64_t* wbase = lds + (size_t)wv * gen_wave_words(a.swp);
   uint32_t* off = reinterpret_cast<uint32_t*>(wbase + 64 * a.swp);
   uint32_t* wrt = off + 64;
+  uint32_t* ovi = wrt + 64;
   encode_prologue(lut, wbase, 64 * a.swp);
 
   const uint64_t nwaves = (g.nblocks + 63) / 64;
@@ -295,19 +382,25 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   const bool live = w < nwaves;
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
+  const bool act = live && b < g.nblocks;
 
-  uint32_t len = 0;
-  if (live && b < g.nblocks) {
+  // code the lane's block into `os`: the LDS slot, or an overflow slot
+  // (inlined at both sites: the LDS copy must keep its ds_or writes)
+  auto code = [&](OrSlot& os) __attribute__((always_inline)) -> uint32_t {
     S v[64];
     BlockPos p = block_pos(g, b, D);
-    OrSlot os{wbase + (size_t)lane * a.swp, 2 * a.swp - 1};
     if constexpr (D == 3 && !kIntField<S>) {
       gather3<S, VEC>(v, data, g, p);
-      len = encode_block3<S, REV, false, HI>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
+      return encode_block3<S, REV, false, HI>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
     } else {
       gather_n<S, D>(v, data, g, p);
-      len = encode_block_n<S, D, REV>(os, lut, v, cp);
+      return encode_block_n<S, D, REV>(os, lut, v, cp);
     }
+  };
+  uint32_t len = 0;
+  if (act) {
+    OrSlot os{wbase + (size_t)lane * a.swp, 2 * a.swp - 1};
+    len = code(os);
   }
   const uint32_t incl = wave_incl_scan(len);
   const uint32_t excl_l = incl - len;
@@ -341,10 +434,34 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
   }
   if (!live)
     return;
+  // Blocks longer than their short LDS slot (wave-uniform, rare on smooth
+  // data): coded again into full-size overflow slots, after the look-back so
+  // that no successor waits for it.
+  const bool over = a.ovf && act && len > a.cap_bits;
+  const bool spill = __any(over);
+  if (spill) {
+    uint32_t oi = kNoSlot;
+    if (over) {
+      oi = take_overflow_slot(a);
+      if (oi != kNoSlot) {
+        uint64_t* gs = a.ovf + (size_t)oi * a.ovf_swp;
+        zero_words(gs, a.ovf_swp);
+        OrSlot os{gs, 2 * a.ovf_swp - 1};
+        code(os);
+        wrt[lane] = len < 64 * a.ovf_swp ? len : 64 * a.ovf_swp;
+      }
+    }
+    ovi[lane] = oi;
+  }
   // off/wrt and the slots are this wave's own: LDS ops of a wave complete in order
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-  pack_wave<64>(a, wbase, off, wrt, w, start, total);
+  if (spill) {
+    __threadfence();  // the overflow slots' atomics have landed before they are read
+    pack_wave<64, true>(a, wbase, off, wrt, ovi, w, start, total);
+  } else {
+    pack_wave<64, false>(a, wbase, off, wrt, ovi, w, start, total);
+  }
 }
 
 // Pack the NB block slots of one wave (bit lengths wrt[], bit offsets off[]
@@ -352,9 +469,11 @@ __global__ __launch_bounds__(256) void encode3_general(const S* __restrict__ dat
 // G = g0 + start: interior words are plain stores, the first and last word
 // (shared with the neighbouring waves) go to the partials for the fix-up
 // kernels.  Shared by encode3_general (NB = 64) and encode4 (NB = 16).
-template <int NB>
+// OVF: some blocks of the wave sit in overflow slots (ovi[l] != kNoSlot).
+template <int NB, bool OVF>
 __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
-                                          const uint32_t* wrt, uint64_t w, uint64_t start, uint32_t total)
+                                          const uint32_t* wrt, const uint32_t* ovi, uint64_t w, uint64_t start,
+                                          uint32_t total)
 {
   const int lane = threadIdx.x & 63;
   const uint64_t G = a.g0 + start;
@@ -385,8 +504,15 @@ __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* 
       int64_t s1 = s0 + wrt[l];
       int64_t x0 = s0 > lo ? s0 : lo;
       int64_t x1 = s1 < hi ? s1 : hi;
-      if (x0 < x1)
-        val |= slot_bits(wbase + (size_t)l * a.swp, (uint32_t)(x0 - s0), (uint32_t)(x1 - x0)) << (x0 - lo);
+      if (x0 < x1) {
+        const uint32_t sp = (uint32_t)(x0 - s0), cnt = (uint32_t)(x1 - x0);
+        uint64_t bits;
+        if (OVF && ovi[l] != kNoSlot)
+          bits = slot_bits_l2(a.ovf + (size_t)ovi[l] * a.ovf_swp, sp, cnt);
+        else
+          bits = slot_bits(wbase + (size_t)l * a.swp, sp, cnt);
+        val |= bits << (x0 - lo);
+      }
     }
     bool head = (o == 0) && (r0 != 0 || (nw == 1 && (end & 63)));
     bool tail = (o == nw - 1) && (end & 63);
@@ -446,14 +572,26 @@ struct DecodeArgs {
   uint32_t wmagic;         // ceil(2^32 / W)
   const uint16_t* idx_len;
   const uint64_t* idx_base;
+  // Short LDS slots (variable rate): a block longer than cap_bits is staged
+  // into an overflow slot of ovf_W words in global memory instead.
+  uint64_t* ovf;
+  uint32_t* ovf_count;
+  uint32_t* error;       // bit 1: overflow pool exhausted (the host redoes the launch)
+  uint32_t ovf_cap;
+  uint32_t ovf_W;
+  uint32_t cap_bits;
 };
 
 // Each lane's block is staged into its own LDS slot (odd stride: lanes reading
 // the same offset of their blocks hit different banks), funnel-shifted so the
 // block starts at bit 0.  Staging is cooperative: thread t copies word j of
 // block l for t = l*W + j, so consecutive threads read consecutive stream words.
-template <typename S, bool VEC, bool REV, bool HI = false, int D = 3>
-__global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
+// SHORT: short staging slots with the global overflow path (instantiated for
+// the f64 planes-32..63 decoder only, which then fits three waves per SIMD; a
+// second inlined decoder costs the others registers).
+template <typename S, bool VEC, bool REV, bool HI = false, int D = 3, bool SHORT = false>
+__global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ data, Geometry g, CodecParams cp,
+                                                             DecodeArgs a)
 {
   __shared__ uint32_t sq[256];
   __shared__ uint32_t sbit[kWavesPerGroup * 64];
@@ -469,10 +607,10 @@ __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g,
   const bool act = b < g.nblocks;
 
   uint64_t start = 0;
-  uint32_t pos = 0;
+  uint32_t pos = 0, len = 0;
   if (!live) {
   } else if (a.var) {
-    uint32_t len = act ? a.idx_len[b] : 0u;
+    len = act ? a.idx_len[b] : 0u;
     uint32_t incl = wave_incl_scan(len);
     pos = incl - len;
     start = a.idx_base[w];
@@ -507,21 +645,56 @@ __global__ __launch_bounds__(256) void decode3(S* __restrict__ data, Geometry g,
     const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
     wslot[(size_t)l * a.swp + j] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
   }
+  // Blocks longer than a short slot (wave-uniform, rare on smooth data): the
+  // lane stages its whole block into an overflow slot in global memory.
+  const bool over = SHORT && act && len > a.cap_bits;
+  uint64_t* gs = nullptr;
+  if (__any(over) && over) {
+    const uint32_t oi = atomicAdd(a.ovf_count, 1u);
+    if (oi < a.ovf_cap) {
+      gs = a.ovf + (size_t)oi * a.ovf_W;
+      const uint32_t sb = sbit[threadIdx.x];
+      const uint32_t sh = sb & 63;
+      for (uint32_t j = 0; j < a.ovf_W; j++) {
+        const uint64_t gw = W0 + (sb >> 6) + j;
+        const uint64_t lo = gw < a.in_words ? a.in[gw] : 0ull;
+        const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
+        gs[j] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+      }
+    } else {
+      atomicOr(a.error, 2u);
+    }
+  }
   __syncthreads();
   if (!act)
     return;
+  const BlockPos p = block_pos(g, b, D);
+  // (inlined at both sites: the LDS copy must keep its ds_read accesses)
+  auto dec = [&](WordReader& r) __attribute__((always_inline)) {
+    S v[64];
+    if constexpr (D == 3 && !kIntField<S>) {
+      decode_block3<S, REV, HI>(r, sq, v, cp);
+      scatter3<S, VEC>(v, data, g, p);
+    } else {
+      decode_block_n<S, D, REV>(r, sq, v, cp);
+      scatter_n<S, D>(v, data, g, p);
+    }
+  };
+  if (SHORT && __any(over)) {
+    if (over) {
+      if (gs) {
+        WordReader r;
+        r.w = gs;
+        r.pos = 0;
+        dec(r);
+      }
+      return;
+    }
+  }
   WordReader r;
   r.w = wslot + (size_t)lane * a.swp;
   r.pos = 0;
-  S v[64];
-  const BlockPos p = block_pos(g, b, D);
-  if constexpr (D == 3 && !kIntField<S>) {
-    decode_block3<S, REV, HI>(r, sq, v, cp);
-    scatter3<S, VEC>(v, data, g, p);
-  } else {
-    decode_block_n<S, D, REV>(r, sq, v, cp);
-    scatter_n<S, D>(v, data, g, p);
-  }
+  dec(r);
 }
 
 }  // namespace zfp_amd

@@ -28,7 +28,19 @@ constexpr uint32_t kDec4HeadWords = (64 + 16) / 2;
 // wave start on different banks.
 __host__ __device__ constexpr uint32_t slot_words4(uint32_t lim) { return ((((lim + 31u) >> 5) + 3u) / 2u) | 1u; }
 
-template <typename S, bool VEC, bool REV>
+// Overflow list of the short-slot 4D encoder: a block longer than its LDS slot
+// is packed with its first cap_bits only (the rest zero) and listed with its
+// stream bit position; encode4_patch codes it again with a full-size slot and
+// ORs it in.  The list lives in GeneralArgs::ovf (two words per entry).
+struct OvfEntry {
+  uint64_t b;    // block
+  uint64_t pos;  // bit position of its first bit relative to out[0]
+};
+
+// HALF: exchange areas shared by quads q and q + 8 (block4.h exchange_fwd), so
+// the LDS region is max(16 slots, 8 exchange areas); with a.ovf the slots are
+// short (see OvfEntry).
+template <typename S, bool VEC, bool REV, bool HALF = false>
 __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geometry g, CodecParams cp, GeneralArgs a)
 {
   using Int = typename Traits<S>::Int;
@@ -72,24 +84,25 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   }
   __syncthreads();
   uint32_t* d = reinterpret_cast<uint32_t*>(region + (size_t)qd * a.swp);
-  Int* X = reinterpret_cast<Int*>(region) + (size_t)qd * kXStride;
-  uint32_t len = encode_block4<S, REV>(d, 2 * a.swp - 1, lut, tab, X, region, kBlocks4PerWave * a.swp, v, cp,
-                                       [&](S (&rr)[64]) {
-                                         if (valid) {
-                                           gather3<S, VEC>(rr, data, g, ps);
-                                         } else {
+  Int* X = reinterpret_cast<Int*>(region) + (size_t)(HALF ? (qd & 7u) : qd) * kXStride;
+  uint32_t len = encode_block4<S, REV, HALF>(d, 2 * a.swp - 1, lut, tab, X, region, kBlocks4PerWave * a.swp, v, cp,
+                                             [&](S (&rr)[64]) {
+                                               if (valid) {
+                                                 gather3<S, VEC>(rr, data, g, ps);
+                                               } else {
 #pragma unroll
-                                           for (int i = 0; i < 64; i++)
-                                             rr[i] = 0;
-                                         }
-                                       });
+                                                 for (int i = 0; i < 64; i++)
+                                                   rr[i] = 0;
+                                               }
+                                             });
   len = valid ? len : 0u;
+  const bool over = a.ovf && len > a.cap_bits;  // quad-uniform
   const uint32_t lq = r == 0u ? len : 0u;  // the quad's lanes agree on len
   const uint32_t incl = wave_incl_scan(lq);
   const uint32_t total = __shfl(incl, 63, 64);
   if (r == 0u) {
     off[qd] = incl - lq;
-    wrt[qd] = len < 64 * a.swp ? len : 64 * a.swp;
+    wrt[qd] = over ? a.cap_bits : (len < 64 * a.swp ? len : 64 * a.swp);
   }
   uint64_t start = 0;
   if (!live) {
@@ -106,10 +119,81 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   } else {
     start = first * (uint64_t)a.maxbits;
   }
+  if (over && r == 0u) {
+    const uint32_t k = take_overflow_slot(a);
+    if (k != kNoSlot)
+      reinterpret_cast<OvfEntry*>(a.ovf)[k] = OvfEntry{b, a.g0 + start + (incl - lq)};
+  }
   __syncthreads();
   if (!live)
     return;
-  pack_wave<kBlocks4PerWave>(a, region, off, wrt, w, start, total);
+  pack_wave<kBlocks4PerWave, false>(a, region, off, wrt, nullptr, w, start, total);
+}
+
+// Second pass of a short-slot encode4: the listed blocks (n entries, 16 per
+// wave), each coded with a full-size slot and ORed into the stream at its
+// recorded position (its first cap_bits are already there; OR is idempotent
+// on them).
+template <typename S, bool VEC, bool REV>
+__global__ __launch_bounds__(64) void encode4_patch(const S* __restrict__ data, Geometry g, CodecParams cp,
+                                                    uint64_t* __restrict__ out, const OvfEntry* __restrict__ list,
+                                                    uint32_t n, uint32_t swp)
+{
+  using Int = typename Traits<S>::Int;
+  extern __shared__ uint64_t lds[];
+  uint32_t* lut = reinterpret_cast<uint32_t*>(lds);
+  uint32_t* tab = lut + 256;
+  uint64_t* region = lds + kEnc4HeadWords;
+  const uint32_t lane = threadIdx.x;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; i++)
+    lut[lane + 64 * i] = dbl_entry(lane + 64 * i);
+  tab[lane] = kOrderTab4.t[lane];
+  const uint32_t qd = lane >> 2, r = lane & 3u;
+  const uint64_t e = (uint64_t)blockIdx.x * kBlocks4PerWave + qd;
+  const bool valid = e < n;
+  const uint64_t b = valid ? list[e].b : 0ull;
+  BlockPos ps{};
+  S v[64];
+  if (valid) {
+    const BlockPos p = block_pos(g, b, 4);
+    ps = slice_pos(g, p, pad_src_w((int)r, p.cnt[3]));
+    gather3<S, VEC>(v, data, g, ps);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; i++)
+      v[i] = 0;
+  }
+  __syncthreads();
+  uint32_t* d = reinterpret_cast<uint32_t*>(region + (size_t)qd * swp);
+  Int* X = reinterpret_cast<Int*>(region) + (size_t)qd * kXStride;
+  const uint32_t len = encode_block4<S, REV>(d, 2 * swp - 1, lut, tab, X, region, kBlocks4PerWave * swp, v, cp,
+                                             [&](S (&rr)[64]) {
+                                               if (valid) {
+                                                 gather3<S, VEC>(rr, data, g, ps);
+                                               } else {
+#pragma unroll
+                                                 for (int i = 0; i < 64; i++)
+                                                   rr[i] = 0;
+                                               }
+                                             });
+  __syncthreads();
+  if (!valid)
+    return;
+  const uint64_t pos = list[e].pos;
+  const uint32_t r0 = (uint32_t)(pos & 63);
+  const uint32_t bits = len < 64 * swp ? len : 64 * swp;  // beyond the slot: minbits padding zeros
+  const uint32_t nw = (r0 + bits + 63) >> 6;
+  const uint64_t* slot = region + (size_t)qd * swp;
+  for (uint32_t k = r; k < nw; k += 4) {
+    const int64_t lo = (int64_t)k * 64 - r0;  // block bit at the word's bit 0
+    const int64_t x0 = lo > 0 ? lo : 0;
+    const int64_t x1 = lo + 64 < (int64_t)bits ? lo + 64 : (int64_t)bits;
+    if (x0 < x1) {
+      const uint64_t val = slot_bits(slot, (uint32_t)x0, (uint32_t)(x1 - x0)) << (x0 - lo);
+      atomicOr((unsigned long long*)&out[(pos >> 6) + k], (unsigned long long)val);
+    }
+  }
 }
 
 template <typename S, bool VEC, bool REV>

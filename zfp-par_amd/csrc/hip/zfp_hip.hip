@@ -116,7 +116,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t side[2] = {nullptr, nullptr};  // host slab pipeline: uploads, downloads
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // [4], [5]: index scan
-  Scratch field, words, status, partials, misc;
+  Scratch field, words, status, partials, misc, ovf;
   Scratch scan_bm, scan_seg, scan_tiles, scan_pos;  // index scan of a stream without index
   zfp_hip_index scan_index;                         // index built by the scan
 };
@@ -142,7 +142,7 @@ static void free_scratch(Scratch& s)
 static void destroy_ctx(Ctx* c)
 {
   (void)hipSetDevice(c->device);
-  for (Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->scan_bm, &c->scan_seg,
+  for (Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->ovf, &c->scan_bm, &c->scan_seg,
                      &c->scan_tiles, &c->scan_pos})
     free_scratch(*s);
   index_release(&c->scan_index);
@@ -412,6 +412,15 @@ static void launch_decode3(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 bl
     if (p.dims == 1) return launch_dec_generic<S, 1>(c, p, d_field, grid, block, lds, a);
     if (p.dims == 2) return launch_dec_generic<S, 2>(c, p, d_field, grid, block, lds, a);
     const bool rev = p.cp.minexp < kMinExp;
+    if constexpr (HI) {
+      if (a.ovf) {  // short staging slots
+        if (p.vec)
+          hipLaunchKernelGGL((decode3<S, true, false, true, 3, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+        else
+          hipLaunchKernelGGL((decode3<S, false, false, true, 3, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+        return;
+      }
+    }
     if (p.vec && rev)
       hipLaunchKernelGGL((decode3<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
     else if (p.vec)
@@ -465,6 +474,9 @@ static int general_args(Ctx* c, const Plan& p, uint64_t nwaves, uint32_t swp, ui
 
 // After a packing encoder: merge the words shared by neighbouring waves; for a
 // variable-rate stream read back its length (and the look-back health flag).
+// kRedoFullSlots: the overflow pool of a short-slot launch ran out, the launch
+// must be repeated with full-size slots.
+constexpr int kRedoFullSlots = 2;
 static int finish_general(Ctx* c, const Plan& p, uint64_t nwaves, uint64_t* d_out, uint32_t g0, const Head& head,
                           const GeneralArgs& a, zfp_hip_index* index, uint64_t* total_bits)
 {
@@ -477,8 +489,11 @@ static int finish_general(Ctx* c, const Plan& p, uint64_t nwaves, uint64_t* d_ou
     uint64_t host[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(host, c->misc.p, 16, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    if ((uint32_t)(host[1] >> 32))
+    const uint32_t err = (uint32_t)(host[1] >> 32);
+    if (err & 1u)
       return fail("zfp_hip: look-back timed out (GPU scheduling anomaly)");
+    if (err & 2u)
+      return kRedoFullSlots;
     *total_bits = host[0];
     if (index)
       index->total_bits = host[0];
@@ -486,6 +501,78 @@ static int finish_general(Ctx* c, const Plan& p, uint64_t nwaves, uint64_t* d_ou
     *total_bits = p.g.nblocks * (uint64_t)p.cp.maxbits;
   }
   return 1;
+}
+
+// Short LDS slots for the variable-rate 3D encoders.  A slot sized for the
+// block's worst case (C3: 2,123 bits, 35 words) limits the CU to two
+// workgroups; the kernels' registers allow three (f64 planes 32..63: <= 168
+// VGPRs) or four (f32 lossy).  The slot is cut to what that
+// many workgroups can hold; blocks that code longer take the overflow pool.
+// Fixed rate, 1D/2D and integer fields keep full-size slots.
+template <typename S>
+static uint32_t short_slot_words(const Plan& p)
+{
+  if (p.fixed || p.dims != 3 || kIntField<S> || getenv("ZFP_HIP_FULL_SLOTS"))
+    return ~0u;
+  const bool rev = p.cp.minexp < kMinExp;
+  // f32 reversible: 177 VGPRs (two waves per SIMD whatever the slots); measured
+  // slower at three with spills
+  int groups;
+  if (sizeof(S) == 4)
+    groups = rev ? 2 : 4;
+  else
+    groups = hi_planes<S>(p) ? 3 : 2;
+  if (const char* e = getenv("ZFP_HIP_SLOT_WORDS"))  // tests: force overflows
+    return (uint32_t)atoi(e) | 1u;
+  const int64_t words = ((int64_t)(160 * 1024) / groups - (int64_t)kLutBytes) / 8 / kWavesPerGroup;
+  int64_t swp = (words - 96) / 64;
+  if ((swp & 1) == 0)
+    swp--;
+  return swp < 3 ? ~0u : (uint32_t)swp;
+}
+
+// Short slots for the variable-rate 4D encoder (f32/f64 fields): the region of
+// 16 slots sized for the worst case (f32 reversible: 8,462 bits, 17.3 KB)
+// limits the CU to 7 workgroups (< 2 waves per SIMD); the registers allow 3
+// (f32 reversible, 145 VGPRs) or 4 (f32 lossy).  The exchange areas are halved
+// (HALF), the slots cut to what is left; longer blocks go to encode4_patch.
+template <typename S>
+static uint32_t short_slot_words4(const Plan& p)
+{
+  if (p.fixed || kIntField<S> || sizeof(S) == 8 || getenv("ZFP_HIP_FULL_SLOTS"))
+    return ~0u;
+  if (const char* e = getenv("ZFP_HIP_SLOT_WORDS"))  // tests: force overflows
+    return (uint32_t)atoi(e) | 1u;
+  const bool rev = p.cp.minexp < kMinExp;
+  const int groups = rev ? 3 : 4;
+  const int64_t region = (int64_t)(160 * 1024) / groups - (int64_t)kEnc4HeadWords * 8;
+  int64_t swp = region / (8 * kBlocks4PerWave);
+  if ((swp & 1) == 0)
+    swp--;
+  return swp < 5 ? ~0u : (uint32_t)swp;
+}
+
+template <typename S>
+static void launch_encode4_kernel(Ctx* c, const Plan& p, const S* d_field, dim3 grid, size_t lds, const GeneralArgs& a,
+                                  bool half)
+{
+  const bool rev = p.cp.minexp < kMinExp;
+  if constexpr (kIntField<S>) {
+    launch_encode4_int(p.type, rev, p.vec, c->stream, grid, dim3(64), lds, d_field, p.g, p.cp, a);
+  } else {
+#define ZFP_ENC4(V, R)                                                                                      \
+  do {                                                                                                      \
+    if (half)                                                                                               \
+      hipLaunchKernelGGL((encode4<S, V, R, true>), grid, dim3(64), lds, c->stream, d_field, p.g, p.cp, a);  \
+    else                                                                                                    \
+      hipLaunchKernelGGL((encode4<S, V, R, false>), grid, dim3(64), lds, c->stream, d_field, p.g, p.cp, a); \
+  } while (0)
+    if (p.vec && rev) ZFP_ENC4(true, true);
+    else if (p.vec) ZFP_ENC4(true, false);
+    else if (rev) ZFP_ENC4(false, true);
+    else ZFP_ENC4(false, false);
+#undef ZFP_ENC4
+  }
 }
 
 // 4D: encode4 for every mode (one 64-thread workgroup per 16 blocks)
@@ -497,31 +584,64 @@ static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_o
   const uint64_t nwaves = (p.g.nblocks + kBlocks4PerWave - 1) / kBlocks4PerWave;
   if (nwaves > 0x7fffffffull)
     return fail("zfp_hip: field too large for one launch");
-  const uint32_t swp = slot_words4(p.bound_bits);
-  const size_t region = std::max<size_t>((size_t)kBlocks4PerWave * swp * 8,
-                                         (size_t)kBlocks4PerWave * kXStride * sizeof(Int));
-  const size_t lds = (size_t)kEnc4HeadWords * 8 + region;
-  if (lds > 160 * 1024)
-    return fail("zfp_hip: 4D block bound %u bits too large for LDS", p.bound_bits);
-  GeneralArgs a{};
-  if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
-    return 0;
-  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  dim3 grid((unsigned)nwaves), block(64);
-  const bool rev = p.cp.minexp < kMinExp;
-  if constexpr (kIntField<S>)
-    launch_encode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
-  else if (p.vec && rev)
-    hipLaunchKernelGGL((encode4<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (p.vec)
-    hipLaunchKernelGGL((encode4<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (rev)
-    hipLaunchKernelGGL((encode4<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else
-    hipLaunchKernelGGL((encode4<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  return finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
+  const uint32_t swp_full = slot_words4(p.bound_bits);
+  const size_t xfull = (size_t)kBlocks4PerWave * kXStride * sizeof(Int);
+  const bool half = !kIntField<S>;  // f32/f64: exchange areas shared by two quads
+  const uint32_t swp_short = short_slot_words4<S>(p);
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const uint32_t swp = attempt == 0 ? std::min(swp_full, swp_short) : swp_full;
+    const size_t region = std::max<size_t>((size_t)kBlocks4PerWave * swp * 8, half ? xfull / 2 : xfull);
+    const size_t lds = (size_t)kEnc4HeadWords * 8 + region;
+    if (lds > 160 * 1024)
+      return fail("zfp_hip: 4D block bound %u bits too large for LDS", p.bound_bits);
+    GeneralArgs a{};
+    if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
+      return 0;
+    if (swp < swp_full) {
+      uint64_t cap = std::min<uint64_t>(p.g.nblocks, std::max<uint64_t>(16384, p.g.nblocks / 16));
+      if (const char* e = getenv("ZFP_HIP_OVF_POOL"))
+        cap = std::max<uint64_t>(1, std::min<uint64_t>(cap, (uint64_t)atoll(e)));
+      if (!ensure(c->ovf, cap * sizeof(OvfEntry)))
+        return 0;
+      a.ovf = (uint64_t*)c->ovf.p;
+      a.ovf_count = (uint32_t*)((char*)c->misc.p + 16);
+      a.ovf_cap = (uint32_t)cap;
+      a.ovf_swp = swp_full;
+      a.cap_bits = 32 * (2 * swp - 2);  // clamped writes of an outrun slot land in its last dword
+    }
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    launch_encode4_kernel<S>(c, p, d_field, dim3((unsigned)nwaves), lds, a, half);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    const int rc = finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
+    if (rc == kRedoFullSlots)
+      continue;
+    if (rc != 1 || !a.ovf)
+      return rc;
+    if constexpr (!kIntField<S>) {
+      uint32_t n = 0;
+      HIP_TRY(hipMemcpyAsync(&n, a.ovf_count, 4, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      if (n) {
+        const size_t plds = (size_t)kEnc4HeadWords * 8 + std::max<size_t>((size_t)kBlocks4PerWave * swp_full * 8, xfull);
+        const dim3 pg((n + kBlocks4PerWave - 1) / kBlocks4PerWave), pb(64);
+        const OvfEntry* list = (const OvfEntry*)a.ovf;
+        const bool rev = p.cp.minexp < kMinExp;
+        if (p.vec && rev)
+          hipLaunchKernelGGL((encode4_patch<S, true, true>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
+        else if (p.vec)
+          hipLaunchKernelGGL((encode4_patch<S, true, false>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
+        else if (rev)
+          hipLaunchKernelGGL((encode4_patch<S, false, true>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
+        else
+          hipLaunchKernelGGL((encode4_patch<S, false, false>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+      }
+    }
+    return 1;
+  }
+  return fail("zfp_hip: overflow pool exhausted with full-size slots");
 }
 
 template <typename S>
@@ -571,25 +691,45 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
     return 1;
   }
   // general path
-  const uint32_t swp = (uint32_t)slot_words_odd(p.bound_bits);
-  size_t lds = (size_t)kWavesPerGroup * (64 * swp + 64) * 8;
-  if (lds + kLutBytes > 160 * 1024)
-    return fail("zfp_hip: block bound %u bits too large for LDS", p.bound_bits);
-  GeneralArgs a{};
-  if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
-    return 0;
-  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  if constexpr (sizeof(S) == 8) {
-    if (hi_planes<S>(p))
-      launch_general3<S, true>(c, p, d_field, grid, block, lds, a);
-    else
+  const uint32_t swp_full = (uint32_t)slot_words_odd(p.bound_bits);
+  const uint32_t swp_short = short_slot_words<S>(p);
+  for (int attempt = 0; attempt < 2; attempt++) {
+    const uint32_t swp = attempt == 0 ? std::min(swp_full, swp_short) : swp_full;
+    size_t lds = (size_t)kWavesPerGroup * gen_wave_words(swp) * 8;
+    if (lds + kLutBytes > 160 * 1024)
+      return fail("zfp_hip: block bound %u bits too large for LDS", p.bound_bits);
+    GeneralArgs a{};
+    if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
+      return 0;
+    if (swp < swp_full) {
+      // overflow pool: a sixteenth of the blocks (at least 64K, at most all)
+      uint64_t cap = std::min<uint64_t>(p.g.nblocks, std::max<uint64_t>(65536, p.g.nblocks / 16));
+      if (const char* e = getenv("ZFP_HIP_OVF_POOL"))  // tests: force the full-slot redo
+        cap = std::max<uint64_t>(1, std::min<uint64_t>(cap, (uint64_t)atoll(e)));
+      if (!ensure(c->ovf, cap * swp_full * 8))
+        return 0;
+      a.ovf = (uint64_t*)c->ovf.p;
+      a.ovf_count = (uint32_t*)((char*)c->misc.p + 16);
+      a.ovf_cap = (uint32_t)cap;
+      a.ovf_swp = swp_full;
+      a.cap_bits = 64 * swp - 96;  // the clamped writes of an outrun slot land in its last three dwords
+    }
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    if constexpr (sizeof(S) == 8) {
+      if (hi_planes<S>(p))
+        launch_general3<S, true>(c, p, d_field, grid, block, lds, a);
+      else
+        launch_general3<S, false>(c, p, d_field, grid, block, lds, a);
+    } else {
       launch_general3<S, false>(c, p, d_field, grid, block, lds, a);
-  } else {
-    launch_general3<S, false>(c, p, d_field, grid, block, lds, a);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    const int rc = finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
+    if (rc != kRedoFullSlots)
+      return rc;
   }
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  return finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
+  return fail("zfp_hip: overflow pool exhausted with full-size slots");
 }
 
 template <typename S>
@@ -640,6 +780,26 @@ static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_i
   return 1;
 }
 
+// Short staging slots for the variable-rate 3D decoder (the encoder's rule,
+// short_slot_words): words staged per block such that the kernel's VGPR-bound
+// number of workgroups fits the CU's LDS; longer blocks are staged in global
+// memory.  ~0u: full size.
+template <typename S>
+static uint32_t short_stage_words(const Plan& p)
+{
+  if (p.fixed || p.dims != 3 || kIntField<S> || getenv("ZFP_HIP_FULL_SLOTS"))
+    return ~0u;
+  if (!hi_planes<S>(p))  // the only decoder instantiated with short slots
+    return ~0u;
+  if (const char* e = getenv("ZFP_HIP_SLOT_WORDS"))  // tests: force overflows
+    return (uint32_t)atoi(e) | 1u;
+  const int groups = 3;
+  const int64_t words = ((int64_t)(160 * 1024) / groups - (int64_t)kLutBytes - kWavesPerGroup * 64 * 4) / 8 /
+                        (kWavesPerGroup * 64);
+  const int64_t W = (words & 1) ? words : words - 1;
+  return W < 3 ? ~0u : (uint32_t)W;
+}
+
 template <typename S>
 static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
                          const zfp_hip_index* index)
@@ -651,36 +811,61 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
     return fail("zfp_hip: block index has %llu waves, the 3D layout needs %llu", (unsigned long long)index->nwaves,
                 (unsigned long long)nwaves);
   const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
-  DecodeArgs a{};
-  a.in = d_in;
-  a.in_words = in_words;
-  a.g0 = g0;
-  a.var = p.fixed ? 0 : 1;
-  a.maxbits = p.cp.maxbits;
-  uint32_t per_block = p.fixed ? p.cp.maxbits : p.max_len;
-  a.W = (per_block + 63) / 64 + 1;  // peek64 at the budget end reads one word past it
-  a.swp = a.W | 1;
-  a.wmagic = (uint32_t)((0x100000000ull + a.W - 1) / a.W);
-  if (!p.fixed) {
-    a.idx_len = index->d_len;
-    a.idx_base = index->d_base;
-  }
-  size_t lds = (size_t)kWavesPerGroup * 64 * a.swp * 8;
-  if (lds + kLutBytes + kWavesPerGroup * 64 * 4 > 160 * 1024)
-    return fail("zfp_hip: block size too large for LDS staging (%u bits)", per_block);
-  dim3 grid((unsigned)ngroups), block(256);
-  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  if constexpr (sizeof(S) == 8) {
-    if (hi_planes<S>(p))
-      launch_decode3<S, true>(c, p, d_field, grid, block, lds, a);
-    else
+  const uint32_t per_block = p.fixed ? p.cp.maxbits : p.max_len;
+  const uint32_t W_full = (per_block + 63) / 64 + 1;  // peek64 at the budget end reads one word past it
+  const uint32_t W_short = short_stage_words<S>(p);
+  for (int attempt = 0; attempt < 2; attempt++) {
+    DecodeArgs a{};
+    a.in = d_in;
+    a.in_words = in_words;
+    a.g0 = g0;
+    a.var = p.fixed ? 0 : 1;
+    a.maxbits = p.cp.maxbits;
+    a.W = attempt == 0 ? std::min(W_full, W_short) : W_full;
+    a.swp = a.W | 1;
+    a.wmagic = (uint32_t)((0x100000000ull + a.W - 1) / a.W);
+    if (!p.fixed) {
+      a.idx_len = index->d_len;
+      a.idx_base = index->d_base;
+    }
+    size_t lds = (size_t)kWavesPerGroup * 64 * a.swp * 8;
+    if (lds + kLutBytes + kWavesPerGroup * 64 * 4 > 160 * 1024)
+      return fail("zfp_hip: block size too large for LDS staging (%u bits)", per_block);
+    if (a.W < W_full) {
+      uint64_t cap = std::min<uint64_t>(p.g.nblocks, std::max<uint64_t>(65536, p.g.nblocks / 16));
+      if (const char* e = getenv("ZFP_HIP_OVF_POOL"))
+        cap = std::max<uint64_t>(1, std::min<uint64_t>(cap, (uint64_t)atoll(e)));
+      if (!ensure(c->ovf, cap * W_full * 8) || !ensure(c->misc, 64))
+        return 0;
+      HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, c->stream));
+      a.ovf = (uint64_t*)c->ovf.p;
+      a.ovf_count = (uint32_t*)((char*)c->misc.p + 16);
+      a.error = (uint32_t*)((char*)c->misc.p + 12);
+      a.ovf_cap = (uint32_t)cap;
+      a.ovf_W = W_full;
+      a.cap_bits = (a.W - 1) * 64;
+    }
+    dim3 grid((unsigned)ngroups), block(256);
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    if constexpr (sizeof(S) == 8) {
+      if (hi_planes<S>(p))
+        launch_decode3<S, true>(c, p, d_field, grid, block, lds, a);
+      else
+        launch_decode3<S, false>(c, p, d_field, grid, block, lds, a);
+    } else {
       launch_decode3<S, false>(c, p, d_field, grid, block, lds, a);
-  } else {
-    launch_decode3<S, false>(c, p, d_field, grid, block, lds, a);
+    }
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    if (!a.ovf)
+      return 1;
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, a.error, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!(err & 2u))
+      return 1;
   }
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  return 1;
+  return fail("zfp_hip: decode overflow pool exhausted with full-size slots");
 }
 
 static void record_timing(Ctx* c)
@@ -1593,7 +1778,7 @@ size_t zfp_hip_scratch_bytes(void)
   std::lock_guard<std::mutex> lk(g_pool_mu);
   size_t b = 0;
   for (Ctx* c : g_idle) {
-    for (const Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->scan_bm, &c->scan_seg,
+    for (const Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->ovf, &c->scan_bm, &c->scan_seg,
                              &c->scan_tiles, &c->scan_pos})
       b += s->bytes;
     b += c->scan_index.cap_blocks * 2 + c->scan_index.cap_waves * 8;

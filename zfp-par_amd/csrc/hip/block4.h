@@ -177,35 +177,48 @@ __device__ __forceinline__ void exchange_fwd(Int (&q)[64], Int* X, const uint32_
 }
 
 // inverse: coefficients in coding order -> inverse w-lift (decode4.c:31-36) ->
-// lane r gets slice w = r
-template <bool REV, typename Int>
+// lane r gets slice w = r.  HALF: as exchange_fwd.
+template <bool REV, bool HALF = false, typename Int>
 __device__ __forceinline__ void exchange_inv(Int (&q)[64], Int* X, const uint32_t* tab)
 {
   const uint32_t r = threadIdx.x & 3u;
+  const uint32_t mine_h = (threadIdx.x >> 5) & 1u;
   __syncthreads();
+#pragma unroll 1
+  for (uint32_t h = 0; h < (HALF ? 2u : 1u); h++) {
+    const bool mine = !HALF || mine_h == h;
+    if (mine) {
 #pragma unroll
-  for (int m = 0; m < 16; m++) {
-    const uint32_t t = tab[16 * r + m];
+      for (int m = 0; m < 16; m++) {
+        const uint32_t t = tab[16 * r + m];
 #pragma unroll
-    for (int i = 0; i < 4; i++)
-      X[(t >> (8 * i)) & 0xffu] = q[4 * m + i];
+        for (int i = 0; i < 4; i++)
+          X[(t >> (8 * i)) & 0xffu] = q[4 * m + i];
+      }
+    }
+    __syncthreads();
+    if (mine) {
+#pragma unroll
+      for (int j = 0; j < 16; j++) {
+        Int* e = X + 4 * (16 * r + j);
+        Int a = e[0], b = e[1], c = e[2], d = e[3];
+        if (REV) Lift<Int>::rinv(a, b, c, d);
+        else Lift<Int>::inv(a, b, c, d);
+        e[0] = a;
+        e[1] = b;
+        e[2] = c;
+        e[3] = d;
+      }
+    }
+    __syncthreads();
+    if (mine) {
+#pragma unroll
+      for (int i = 0; i < 64; i++)
+        q[i] = X[4 * i + r];
+    }
+    if (HALF)
+      __syncthreads();
   }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < 16; j++) {
-    Int* e = X + 4 * (16 * r + j);
-    Int a = e[0], b = e[1], c = e[2], d = e[3];
-    if (REV) Lift<Int>::rinv(a, b, c, d);
-    else Lift<Int>::inv(a, b, c, d);
-    e[0] = a;
-    e[1] = b;
-    e[2] = c;
-    e[3] = d;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 64; i++)
-    q[i] = X[4 * i + r];
 }
 
 // zero `words` 64-bit words at w (whole wave)
@@ -591,7 +604,7 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
 
 // Decode the quad's block (invalid quads decode nothing but take part in the
 // wave-wide exchange); lane r receives slice w = r.
-template <typename S, bool REV>
+template <typename S, bool REV, bool HALF = false>
 __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const CodecParams& cp,
                                               typename Traits<S>::Int* X, const uint32_t* tab, bool valid)
 {
@@ -622,7 +635,7 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
       else
         coeffs_from_planes<false>(q, P, prec > 32);
     }
-    exchange_inv<REV>(q, X, tab);
+    exchange_inv<REV, HALF>(q, X, tab);
     xform<3, true, REV>(q);
 #pragma unroll
     for (int i = 0; i < 64; i++)
@@ -656,7 +669,7 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
       else
         coeffs_from_planes<false>(q, P, prec > 32);
     }
-    exchange_inv<REV>(q, X, tab);
+    exchange_inv<REV, HALF>(q, X, tab);
     xform<3, true, REV>(q);
     if (REV && kind == 2u) {
 #pragma unroll

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(64) void encode4_patch(const S* __restrict__ data, 
   }
 }
 
-template <typename S, bool VEC, bool REV>
+template <typename S, bool VEC, bool REV, bool HALF = false>
 __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
 {
   using Int = typename Traits<S>::Int;
@@ -254,8 +254,8 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
   rd.w = region + (size_t)qd * a.swp;
   rd.pos = 0;
   S v[64];
-  Int* X = reinterpret_cast<Int*>(region) + (size_t)qd * kXStride;
-  decode_block4<S, REV>(rd, v, cp, X, tab, valid);
+  Int* X = reinterpret_cast<Int*>(region) + (size_t)(HALF ? (qd & 7u) : qd) * kXStride;
+  decode_block4<S, REV, HALF>(rd, v, cp, X, tab, valid);
   if (!valid)
     return;
   const BlockPos p = block_pos(g, b, 4);

@@ -757,8 +757,10 @@ static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_i
     a.idx_len = index->d_len;
     a.idx_base = index->d_base;
   }
-  const size_t region = std::max<size_t>((size_t)kBlocks4PerWave * a.swp * 8,
-                                         (size_t)kBlocks4PerWave * kXStride * sizeof(Int));
+  // f32/f64: exchange areas shared by quad pairs (HALF), as in the encoder
+  const bool half = !kIntField<S>;
+  const size_t xfull = (size_t)kBlocks4PerWave * kXStride * sizeof(Int);
+  const size_t region = std::max<size_t>((size_t)kBlocks4PerWave * a.swp * 8, half ? xfull / 2 : xfull);
   const size_t lds = (size_t)kDec4HeadWords * 8 + region;
   if (lds > 160 * 1024)
     return fail("zfp_hip: 4D block size too large for LDS staging (%u bits)", per_block);
@@ -768,13 +770,13 @@ static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_i
   if constexpr (kIntField<S>)
     launch_decode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
   else if (p.vec && rev)
-    hipLaunchKernelGGL((decode4<S, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    hipLaunchKernelGGL((decode4<S, true, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   else if (p.vec)
-    hipLaunchKernelGGL((decode4<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    hipLaunchKernelGGL((decode4<S, true, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   else if (rev)
-    hipLaunchKernelGGL((decode4<S, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    hipLaunchKernelGGL((decode4<S, false, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   else
-    hipLaunchKernelGGL((decode4<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    hipLaunchKernelGGL((decode4<S, false, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->ev[2], c->stream));
   return 1;

@@ -596,8 +596,11 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
   __shared__ uint32_t sq[256];
   __shared__ uint32_t sbit[kWavesPerGroup * 64];
   extern __shared__ uint64_t lds[];
-  sq[threadIdx.x] = squeeze_entry(threadIdx.x);
   const int lane = threadIdx.x & 63;
+  // every wave writes the whole (identical) table: no workgroup barrier below
+#pragma unroll
+  for (int k = 0; k < 4; k++)
+    sq[lane + 64 * k] = squeeze_entry(lane + 64 * k);
   const int wv = threadIdx.x >> 6;
   uint64_t* wslot = lds + (size_t)wv * 64 * a.swp;
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
@@ -665,7 +668,9 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
       atomicOr(a.error, 2u);
     }
   }
-  __syncthreads();
+  // the staged slots and the table are this wave's own writes
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+  __builtin_amdgcn_wave_barrier();
   if (!act)
     return;
   const BlockPos p = block_pos(g, b, D);

@@ -991,10 +991,13 @@ static uint64_t scan_seg_bits(uint64_t limit)
     if (v >= 64)
       return v & ~63ull;
   }
-  // about 2^18 lanes at most; segments of at least 16 Kbit so that small
-  // streams need few passes
+  // about 2^18 lanes at most; segments of at least 64 Kbit: a speculative
+  // chain resynchronises after ~116-205 Kbit on average, so
+  // shorter segments cost more passes than their shorter parses save
+  // (512^3 f64 precision 32: 69 ms at 16 Kbit, 55 ms at 64 Kbit; 128^4 f32
+  // reversible: 378 -> 205 ms; profiles/r2d_scan_seg.txt)
   uint64_t L = (limit + (1ull << 18) - 1) >> 18;
-  L = std::max<uint64_t>(L, 16384);
+  L = std::max<uint64_t>(L, 65536);
   return (L + 63) & ~63ull;
 }
 

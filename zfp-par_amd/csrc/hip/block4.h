@@ -247,6 +247,15 @@ __device__ __forceinline__ void or64_clamped(uint32_t* d, uint32_t jmax, uint32_
   lds_or32(d + min(j + 1u, jmax), __builtin_amdgcn_alignbit(0u, v1, t));
 }
 
+// v at bit p >= 1: dwords j-1, j, each clamped to jmax
+__device__ __forceinline__ void or32_clamped(uint32_t* d, uint32_t jmax, uint32_t p, uint32_t v)
+{
+  const uint32_t j = (p + 31u) >> 5;
+  const uint32_t t = 0u - p;
+  lds_or32(d + min(j - 1u, jmax), __builtin_amdgcn_alignbit(v, 0u, t));
+  lds_or32(d + min(j, jmax), __builtin_amdgcn_alignbit(0u, v, t));
+}
+
 // doubled-ones expansion of 32 bits (32 + popcount bits <= 64)
 __device__ __forceinline__ uint64_t dbl32(const uint32_t* lut, uint32_t x)
 {
@@ -315,26 +324,38 @@ __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, con
 #else
     // Straight-line for every lane: an inactive lane (or an empty part) ORs
     // zeros at a clamped address, so no per-lane branch (and no exec-mask
-    // bookkeeping in SGPRs) is needed.
+    // bookkeeping in SGPRs) is needed.  Group bits: the expansion of the
+    // segment's xs unit 0 (bits 0..15) is written here; a lane whose xs
+    // reaches past bit 15 (at most three planes per segment: each moves the
+    // frontier by >= 17) writes its whole expansion again in a wave-uniform
+    // branch (OR is idempotent on the unit-0 bits), as code_planes does.
     {
       const uint64_t V = act ? P & S : 0ull;
       or64_clamped(d, jmax, p + base, (uint32_t)V, (uint32_t)(V >> 32));
       const uint32_t gp = p + n;  // the plane's positive group test
       lds_or32(d + min(gp >> 5, jmax), (act && top1 && r == 0u) ? 1u << (gp & 31u) : 0u);
       const uint64_t xs = (act && nr < 64u) ? N >> nr : 0ull;
-      const uint32_t x0 = (uint32_t)xs, x1 = (uint32_t)(xs >> 32);
-      uint64_t E0 = dbl32(lut, x0), E1 = dbl32(lut, x1);
-      const uint32_t L0 = 32u + (uint32_t)__popc(x0);
+      const uint32_t x0 = (uint32_t)xs;
       // top one at xs bit h; its pair starts at h + (c - 1) of the expansion
       const bool top = bl != 0u && base + bl == top1;
       const uint32_t h = bl - 1u - nr;
       const uint32_t t = h + c - 1u;
-      const uint64_t m = top ? (uint64_t)(2u | impl) : 0ull;
-      E0 &= ~(h < 32u ? m << (t & 63u) : 0ull);
-      E1 &= ~(h < 32u ? 0ull : m << ((t - L0) & 63u));
       const uint32_t co = p + 1u + base + nr + cex;
-      or64_clamped(d, jmax, co, (uint32_t)E0, (uint32_t)(E0 >> 32));
-      or64_clamped(d, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
+      const uint32_t m0 = (top && h < 16u) ? ((2u | impl) << (t & 31u)) : 0u;
+      or32_clamped(d, jmax, co, dbl16(lut, x0 & 0xffffu) & ~m0);
+      const bool ext = (xs >> 16) != 0ull;
+      if (__builtin_amdgcn_ballot_w64(ext) != 0) {
+        if (ext) {
+          const uint32_t x1 = (uint32_t)(xs >> 32);
+          uint64_t E0 = dbl32(lut, x0), E1 = dbl32(lut, x1);
+          const uint32_t L0 = 32u + (uint32_t)__popc(x0);
+          const uint64_t m = top ? (uint64_t)(2u | impl) : 0ull;
+          E0 &= ~(h < 32u ? m << (t & 63u) : 0ull);
+          E1 &= ~(h < 32u ? 0ull : m << ((t - L0) & 63u));
+          or64_clamped(d, jmax, co, (uint32_t)E0, (uint32_t)(E0 >> 32));
+          or64_clamped(d, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
+        }
+      }
     }
 #endif
     p = act ? p + dlen : p;

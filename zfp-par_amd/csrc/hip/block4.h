@@ -140,7 +140,7 @@ __device__ __forceinline__ void exchange_fwd(Int (&q)[64], Int* X, const uint32_
 {
   const uint32_t r = threadIdx.x & 3u;
   const uint32_t mine_h = (threadIdx.x >> 5) & 1u;
-#pragma unroll 1
+#pragma unroll
   for (uint32_t h = 0; h < (HALF ? 2u : 1u); h++) {
     const bool mine = !HALF || mine_h == h;
     if (mine) {
@@ -184,7 +184,7 @@ __device__ __forceinline__ void exchange_inv(Int (&q)[64], Int* X, const uint32_
   const uint32_t r = threadIdx.x & 3u;
   const uint32_t mine_h = (threadIdx.x >> 5) & 1u;
   __syncthreads();
-#pragma unroll 1
+#pragma unroll
   for (uint32_t h = 0; h < (HALF ? 2u : 1u); h++) {
     const bool mine = !HALF || mine_h == h;
     if (mine) {

@@ -218,13 +218,27 @@ struct WordReader {
   const uint64_t* w;
   uint32_t pos;  // bit position within the lane's slot (slots are small)
 
-  // Branch-free 64-bit window at bit p: both words are always read (the slot
-  // has a spare word past its last), and (b << 1) << (63 - s) vanishes at s = 0.
+#ifndef ZFP_PEEK_DWORDS
+#define ZFP_PEEK_DWORDS 1
+#endif
+  // Branch-free 64-bit window at bit p.  Dword form: the three dwords from
+  // dword p/32 on, funnel-shifted by p % 32 (two v_alignbit_b32; a 64-bit
+  // shift costs about three times a 32-bit op); they stay inside the slot,
+  // which has a spare word past its last.  Word form: both words are always
+  // read, and (b << 1) << (63 - s) vanishes at s = 0.
   __device__ __forceinline__ uint64_t peek_at(uint32_t p) const
   {
+#if ZFP_PEEK_DWORDS
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(w) + (p >> 5);
+    const uint32_t s = p & 31u;
+    const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
+    const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, s), hi = __builtin_amdgcn_alignbit(d2, d1, s);
+    return ((uint64_t)hi << 32) | lo;
+#else
     const uint32_t i = p >> 6, s = p & 63u;
     const uint64_t a = w[i], b = w[i + 1];
     return (a >> s) | ((b << 1) << (63u - s));
+#endif
   }
   __device__ __forceinline__ uint64_t peek64() const { return peek_at(pos); }
   __device__ __forceinline__ uint64_t read(uint32_t n)

@@ -22,8 +22,9 @@ timeout -k 10 200 python tools/kprof.py --dims 4 --n 128 --mode rate --param 8 -
 grep -v amdgpu.ids $OUT/kprof_$TAG.txt
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$TAG -o run -- \
-  python $R/bench.py --steps 10 --warmup 10 --no-cpu > $OUT/prof_$TAG.log 2>&1 || { echo prof failed; exit 1; }
+  python $R/bench.py --steps 20 --warmup 10 --no-cpu > $OUT/prof_$TAG.log 2>&1 || { echo prof failed; exit 1; }
 echo prof ok
+python $R/tools/prof_tail.py $OUT/prof_$TAG 20 > $OUT/prof_tail_$TAG.csv && cat $OUT/prof_tail_$TAG.csv
 bash $R/tools/pmc_round.sh ${TAG}_c2 --mode rate --param 16 --decode || exit 1
 bash $R/tools/pmc_round.sh ${TAG}_c3 --mode precision --param 32 --dtype f64 --decode || exit 1
 bash $R/tools/pmc_round.sh ${TAG}_c5 --dims 4 --n 128 --mode reversible --decode || exit 1

@@ -143,3 +143,22 @@ def test_short_slots_and_patch_pass_match_oracle_4d(product, oracle, monkeypatch
     assert n == len(got)
     assert out.tobytes() == ref_out.tobytes()
     _free_index(product)
+
+
+@pytest.mark.parametrize("pack_words", [None, "1100"])
+@pytest.mark.parametrize("mode,param", [("precision", 20), ("accuracy", 1e-3), ("reversible", None)])
+def test_packed_staging_decode_matches_oracle_4d(product, oracle, monkeypatch, pack_words, mode, param):
+    """Variable-rate decode4 stages each wave's blocks back to back; waves
+    whose segment exceeds the LDS (forced with 1100 words on the rough half
+    of the field) make the library repeat the launch with padded slots."""
+    if pack_words:
+        monkeypatch.setenv("ZFP_HIP_PACK_WORDS", pack_words)
+    rng = np.random.default_rng(zlib.crc32(repr((pack_words, mode, param, 44)).encode()))
+    a = _field4((12, 9, 16, 20), np.float32, rng)
+    a[6:] = np.cos(np.arange(6 * 9 * 16 * 20, dtype=np.float32) * 1e-3).reshape(6, 9, 16, 20)
+    want, end = _oracle_bytes(oracle, a, mode, param)
+    params = _params(mode, param, TYPE_FLOAT, a.ndim)
+    ref_out, _ = oracle.decompress_words(np.frombuffer(want, dtype=np.uint64), a.shape, np.float32, params)
+    out, n = product.decompress(want, a.shape, np.float32, mode, param, ztype=TYPE_FLOAT)  # scan-built index
+    assert n == len(want)
+    assert out.tobytes() == ref_out.tobytes()

@@ -580,6 +580,9 @@ struct DecodeArgs {
   uint32_t ovf_cap;
   uint32_t ovf_W;
   uint32_t cap_bits;
+  // decode4, variable rate: the wave's blocks staged back to back (packw words
+  // of LDS at most; 0: one padded slot per block)
+  uint32_t packw;
 };
 
 // Each lane's block is staged into its own LDS slot (odd stride: lanes reading

@@ -229,7 +229,28 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
   const uint64_t left = g.nblocks - first;
   const uint32_t nb = left < kBlocks4PerWave ? (uint32_t)left : kBlocks4PerWave;
   const uint32_t pairs = nb * a.W;
-  if (!a.var && (G & 63) == 0 && (a.maxbits & 63) == 0) {
+  uint32_t rpos = 0;  // the quad's first bit in its staged words
+  const uint64_t* rbase = region + (size_t)qd * a.swp;
+  if (a.packw) {
+    // Packed (variable rate): the wave's blocks are contiguous in the stream,
+    // so its segment is staged as is, one word per lane and step, and each
+    // quad reads its block at its bit offset -- no slot sized for the worst
+    // block.  A segment longer than the LDS holds (rough data) sets the error
+    // flag; the host repeats the launch with padded slots.
+    const uint32_t total = __shfl(pos + (r == 0u && valid ? (uint32_t)a.idx_len[b] : 0u), 4 * (nb - 1), 64);
+    const uint32_t nwords = ((uint32_t)(G & 63) + total + 63) / 64 + 1;  // + 1: the window reads past the end
+    if (nwords > a.packw) {
+      if (lane == 0)
+        atomicOr(a.error, 2u);
+      return;  // wave-uniform: a one-wave workgroup
+    }
+    for (uint32_t t = lane; t < nwords; t += 64) {
+      const uint64_t gw = W0 + t;
+      region[t] = gw < a.in_words ? a.in[gw] : 0ull;
+    }
+    rpos = sbit[qd];
+    rbase = region;
+  } else if (!a.var && (G & 63) == 0 && (a.maxbits & 63) == 0) {
     // word-aligned fixed rate (wave-uniform): block l starts at word l * bw
     const uint32_t bw = a.maxbits >> 6;
     for (uint32_t t = lane; t < pairs; t += 64) {
@@ -251,8 +272,8 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
   }
   __syncthreads();
   WordReader rd;
-  rd.w = region + (size_t)qd * a.swp;
-  rd.pos = 0;
+  rd.w = rbase;
+  rd.pos = rpos;
   S v[64];
   Int* X = reinterpret_cast<Int*>(region) + (size_t)(HALF ? (qd & 7u) : qd) * kXStride;
   decode_block4<S, REV, HALF>(rd, v, cp, X, tab, valid);

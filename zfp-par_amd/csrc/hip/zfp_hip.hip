@@ -760,26 +760,57 @@ static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_i
   // f32/f64: exchange areas shared by quad pairs (HALF), as in the encoder
   const bool half = !kIntField<S>;
   const size_t xfull = (size_t)kBlocks4PerWave * kXStride * sizeof(Int);
-  const size_t region = std::max<size_t>((size_t)kBlocks4PerWave * a.swp * 8, half ? xfull / 2 : xfull);
-  const size_t lds = (size_t)kDec4HeadWords * 8 + region;
-  if (lds > 160 * 1024)
-    return fail("zfp_hip: 4D block size too large for LDS staging (%u bits)", per_block);
-  dim3 grid((unsigned)nwaves), block(64);
-  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-  const bool rev = p.cp.minexp < kMinExp;
-  if constexpr (kIntField<S>)
-    launch_decode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
-  else if (p.vec && rev)
-    hipLaunchKernelGGL((decode4<S, true, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (p.vec)
-    hipLaunchKernelGGL((decode4<S, true, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else if (rev)
-    hipLaunchKernelGGL((decode4<S, false, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  else
-    hipLaunchKernelGGL((decode4<S, false, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-  HIP_TRY(hipGetLastError());
-  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-  return 1;
+  // variable rate, f32/f64: the wave's segment staged back to back in what
+  // three one-wave workgroups per SIMD leave (the decoders' VGPRs allow
+  // three); a wave whose segment does not fit makes the host repeat the
+  // launch with padded slots
+  uint32_t packw = 0;
+  if (!p.fixed && half && !getenv("ZFP_HIP_FULL_SLOTS")) {
+    packw = (uint32_t)(((size_t)(160 * 1024) / 12 - (size_t)kDec4HeadWords * 8) / 8);
+    if (const char* e = getenv("ZFP_HIP_PACK_WORDS"))  // tests: force the redo
+      packw = (uint32_t)atoi(e);
+    if ((size_t)packw * 8 < xfull / 2 || packw >= kBlocks4PerWave * a.swp)
+      packw = 0;
+  }
+  for (int attempt = 0; attempt < 2; attempt++) {
+    a.packw = attempt == 0 ? packw : 0u;
+    const size_t region = a.packw ? std::max<size_t>((size_t)a.packw * 8, xfull / 2)
+                                  : std::max<size_t>((size_t)kBlocks4PerWave * a.swp * 8, half ? xfull / 2 : xfull);
+    const size_t lds = (size_t)kDec4HeadWords * 8 + region;
+    if (lds > 160 * 1024)
+      return fail("zfp_hip: 4D block size too large for LDS staging (%u bits)", per_block);
+    if (a.packw) {
+      if (!ensure(c->misc, 64))
+        return 0;
+      HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, c->stream));
+      a.error = (uint32_t*)((char*)c->misc.p + 12);
+    }
+    dim3 grid((unsigned)nwaves), block(64);
+    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+    const bool rev = p.cp.minexp < kMinExp;
+    if constexpr (kIntField<S>)
+      launch_decode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
+    else if (p.vec && rev)
+      hipLaunchKernelGGL((decode4<S, true, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else if (p.vec)
+      hipLaunchKernelGGL((decode4<S, true, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else if (rev)
+      hipLaunchKernelGGL((decode4<S, false, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    else
+      hipLaunchKernelGGL((decode4<S, false, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+    if (!a.packw)
+      return 1;
+    uint32_t err = 0;
+    HIP_TRY(hipMemcpyAsync(&err, a.error, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (!(err & 2u))
+      return 1;
+    if (getenv("ZFP_HIP_VERBOSE"))
+      fprintf(stderr, "zfp_hip: decode4 segment past %u staged words, repeated with padded slots\n", a.packw);
+  }
+  return fail("zfp_hip: 4D decode staging failed with padded slots");
 }
 
 // Short staging slots for the variable-rate 3D decoder (the encoder's rule,

@@ -764,10 +764,13 @@ static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_i
   // three one-wave workgroups per SIMD leave (the decoders' VGPRs allow
   // three); a wave whose segment does not fit makes the host repeat the
   // launch with padded slots
+  // Off by default: on the C5-mode field (128^4 f32 reversible) some wave of
+  // every call passes the 1,666 words, so every call ran twice
+  // (ZFP_HIP_VERBOSE=1 shows it); a per-wave fallback is the missing piece.
+  // ZFP_HIP_PACK_WORDS=n turns it on with n staged words (tests, tuning).
   uint32_t packw = 0;
   if (!p.fixed && half && !getenv("ZFP_HIP_FULL_SLOTS")) {
-    packw = (uint32_t)(((size_t)(160 * 1024) / 12 - (size_t)kDec4HeadWords * 8) / 8);
-    if (const char* e = getenv("ZFP_HIP_PACK_WORDS"))  // tests: force the redo
+    if (const char* e = getenv("ZFP_HIP_PACK_WORDS"))
       packw = (uint32_t)atoi(e);
     if ((size_t)packw * 8 < xfull / 2 || packw >= kBlocks4PerWave * a.swp)
       packw = 0;

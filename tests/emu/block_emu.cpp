@@ -20,8 +20,15 @@ uint64_t oz_decompress(const oz_job* j, void* data, const uint64_t* words, uint6
 template <typename S>
 static int run(const CodecParams& cp, int type, std::mt19937_64& rng, int trials, const char* name)
 {
-  uint32_t lut[256], sq[256];
-  for (int b = 0; b < 256; b++) lut[b] = dbl_entry(b), sq[b] = squeeze_entry(b);
+  // "LDS" arena: the fixed-rate f32 coder addresses its tables and slot by LDS
+  // byte address (offsets from zfp_emu_lds_base)
+  static std::vector<uint64_t> arena(4096, 0);
+  zfp_emu_lds_base = reinterpret_cast<char*>(arena.data());
+  uint32_t* lut = reinterpret_cast<uint32_t*>(arena.data()) + 64;  // dbl[256], lead[256]
+  uint32_t sq[256];
+  for (int b = 0; b < 256; b++) lut[b] = kCoderTables.dbl[b], lut[256 + b] = kCoderTables.lead[b], sq[b] = squeeze_entry(b);
+  for (int b = 0; b < 256; b++)
+    if (lut[b] != dbl_entry(b)) { printf("CoderTables.dbl[%d] differs from dbl_entry\n", b); return 1; }
   int bad = 0;
   for (int t = 0; t < trials; t++) {
     S v[64], orig[64];
@@ -51,8 +58,9 @@ static int run(const CodecParams& cp, int type, std::mt19937_64& rng, int trials
       // fixed-rate specialisation (the aligned kernel's coder)
       S v2[64];
       for (int i = 0; i < 64; i++) v2[i] = orig[i];
-      std::vector<uint64_t> slot2(600, 0);
-      OrSlot os2{slot2.data(), 1199};
+      uint64_t* slot2 = arena.data() + 1024;  // inside the arena (see above)
+      std::fill(slot2, slot2 + 600, 0ull);
+      OrSlot os2{slot2, 1199};
       uint32_t len2 = encode_block3<S, false, true>(os2, lut, v2, cp, [&](S (&r)[64]) { for (int i = 0; i < 64; i++) r[i] = orig[i]; });
       bool same = len2 == len;
       for (uint32_t i = 0; same && i < (len + 63) / 64; i++) {

@@ -84,10 +84,69 @@ static int run(std::mt19937_64& rng, int trials)
   return bad;
 }
 
+// The fixed-rate f32 coder (code_planes_fr32): its 32-bit plane body runs while
+// the wave's planes have nothing in coefficients 32..63 and n < 32, then it
+// hands over to code_planes.  Patterns keep the high half empty for a varying
+// number of top planes and hit the 32-bit body's edges: xs == 0xffff (33 group
+// bits), tops past bit 15, n reaching 32, empty planes, budgets cut anywhere.
+static int run_fr32(std::mt19937_64& rng, int trials)
+{
+  static std::vector<uint64_t> arena(8192, 0);
+  zfp_emu_lds_base = reinterpret_cast<char*>(arena.data());
+  uint32_t* lut = reinterpret_cast<uint32_t*>(arena.data()) + 64;
+  for (int b = 0; b < 256; b++) lut[b] = kCoderTables.dbl[b], lut[256 + b] = kCoderTables.lead[b];
+  uint64_t* slot = arena.data() + 1024;
+  int bad = 0;
+  for (int t = 0; t < trials; t++) {
+    uint64_t P[32];
+    const int kind = t % 8;
+    const int khi = (int)(rng() % 33);  // planes >= khi: low half only
+    for (int k = 0; k < 32; k++) {
+      uint64_t r = rng();
+      uint64_t lo;
+      switch (kind) {
+        case 0: lo = r & 0xffffffffull; break;
+        case 1: lo = (rng() % 3 == 0) ? r & rng() & 0xffffffffull : 0; break;
+        case 2: lo = (rng() % 4 == 0) ? 0xffffull << (rng() % 17) : (r & 0xffff); break;  // 0xffff units
+        case 3: lo = (rng() % 5 == 0) ? (1ull << 31) : (r & 0xff); break;                  // n jumps to 32
+        case 4: lo = (k % 7 == 0) ? 0xffffffffull : 0; break;
+        case 5: lo = (r & 0xffffffffull) >> (rng() % 32); break;
+        case 6: lo = (k > 24) ? (1ull << (rng() % 32)) : (r & (r >> 5) & 0xffffffffull); break;
+        default: lo = (rng() % 2) ? 0xffff0000ull | (r & 0xffff) : ((r & 0xffff) << 16); break;  // tops past bit 15
+      }
+      P[k] = k >= khi ? lo : (lo | (r & 0xffffffff00000000ull));
+    }
+    uint32_t Pl[32], Ph[32];
+    for (int k = 0; k < 32; k++) Pl[k] = (uint32_t)P[k], Ph[k] = (uint32_t)(P[k] >> 32);
+    const uint32_t pos0 = 1 + (uint32_t)(rng() % 40);
+    const uint32_t budgets[3] = {4096, 64 + (uint32_t)(rng() % 1500), 1 + (uint32_t)(rng() % 300)};
+    for (uint32_t lim_bits : budgets) {
+      std::vector<uint64_t> rw(200, 0);
+      std::fill(slot, slot + 200, 0ull);
+      const uint32_t rlen = ref_code(rw, pos0, lim_bits, 64, P, 32);
+      code_planes_fr32(reinterpret_cast<uint32_t*>(slot), 399, lut, pos0, pos0 + lim_bits, Pl, Ph);
+      const uint32_t e = pos0 + rlen;
+      bool ok = true;
+      for (uint32_t i = 0; ok && i < (e + 63) / 64; i++) {
+        uint64_t m = (i == e / 64 && (e & 63)) ? ((1ull << (e & 63)) - 1) : ~0ull;
+        ok = (slot[i] & m) == (rw[i] & m);
+      }
+      if (!ok && bad++ < 5)
+        printf("fr32 trial %d kind %d khi %d lim %u: stream differs\n", t, kind, khi, lim_bits);
+    }
+  }
+  printf("fr32 mismatches %d\n", bad);
+  return bad;
+}
+
 int main()
 {
   std::mt19937_64 rng(12345);
   int bad = 0;
+  for (int all : {0, 1}) {
+    emu_any_all = all;
+    bad += run_fr32(rng, 40000);
+  }
   for (int all : {0, 1}) {  // 1: every wave-level branch entered (other lanes need it)
     emu_any_all = all;
     bad += run<32, true>(rng, 20000) + run<64, true>(rng, 10000) + run<32, false>(rng, 20000) + run<64, false>(rng, 10000);

@@ -20,6 +20,7 @@ static inline uint64_t __builtin_amdgcn_ballot_w64(bool x) { return (x || emu_an
 static inline int __popc(uint32_t x) { return __builtin_popcount(x); }
 static inline int __popcll(uint64_t x) { return __builtin_popcountll(x); }
 static inline int __clzll(long long x) { return x ? __builtin_clzll((uint64_t)x) : 64; }
+static inline int __clz(int x) { return x ? __builtin_clz((uint32_t)x) : 32; }
 static inline uint32_t __float_as_uint(float f) { uint32_t u; std::memcpy(&u, &f, 4); return u; }
 static inline float __uint_as_float(uint32_t u) { float f; std::memcpy(&f, &u, 4); return f; }
 static inline long long __double_as_longlong(double d) { long long u; std::memcpy(&u, &d, 8); return u; }

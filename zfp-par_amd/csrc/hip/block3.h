@@ -503,7 +503,10 @@ __device__ __forceinline__ void encode_block3_fixed(OrSlot& w, const uint32_t* l
   pin_registers(Pl);
   pin_registers(Ph);
   mid();
-  code_planes<PREC, false>(w, lut, e ? 1 + kE : cp.maxbits, cp.maxbits, mp, Pl, Ph);
+  if constexpr (PREC == 32)  // lut: dbl[256] then lead[256] (CoderTables)
+    code_planes_fr32(w.d(), w.jmax, lut, e ? 1 + kE : cp.maxbits, cp.maxbits, Pl, Ph);
+  else
+    code_planes<PREC, false>(w, lut, e ? 1 + kE : cp.maxbits, cp.maxbits, mp, Pl, Ph);
 }
 
 // Encode one block into a zeroed slot; returns its length in bits including

@@ -185,6 +185,84 @@ __device__ __forceinline__ uint32_t dbl16(const uint32_t* lut, uint32_t u)
   return lut[b0] | (lut[b1] << (8u + (uint32_t)__popc(b0)));
 }
 
+// The coder tables as constants in device memory (a kernel copies them to LDS
+// with one 16-byte load per lane instead of computing them):
+//   dbl[b]  = dbl_entry(b)
+//   lead[b] = (dbl(b) << 1 | 1) << 5 | (9 + popcount(b)): the first byte of a
+//             plane's group bits with the leading "1" test, and in its low five
+//             bits the shift that places the second byte's expansion after it
+//             (code_planes_fr32).
+struct CoderTables {
+  uint32_t dbl[256];
+  uint32_t lead[256];
+  constexpr CoderTables() : dbl(), lead()
+  {
+    for (uint32_t b = 0; b < 256; b++) {
+      uint32_t d = 0, p = 0, c = 0;
+      for (int i = 0; i < 8; i++) {
+        if ((b >> i) & 1u) {
+          d |= 3u << p;
+          p += 2;
+          c++;
+        } else {
+          p += 1;
+        }
+      }
+      dbl[b] = d;
+      lead[b] = (((d << 1) | 1u) << 5) | (9u + c);
+    }
+  }
+};
+static __device__ const CoderTables kCoderTables{};
+
+// ---------------------------------------------------------------------------
+// LDS by byte address: the fixed-rate coder keeps each lane's stream position
+// as a bit address in LDS, so the dword address and the funnel shift of every
+// write come from one register.  (Host emulation: addresses are offsets from
+// zfp_emu_lds_base.)
+#ifdef __HIP_DEVICE_COMPILE__
+typedef __attribute__((address_space(3))) uint32_t lds_dword;
+__device__ __forceinline__ lds_dword* lds_at(uint32_t byte) { return (lds_dword*)(uintptr_t)byte; }
+__device__ __forceinline__ uint32_t lds_off(const void* p) { return (uint32_t)(uintptr_t)p; }
+// (byte k of x) * 4 in one SDWA instruction (the compiler spends a v_mov on the constant)
+__device__ __forceinline__ uint32_t byte0_x4(uint32_t x)
+{
+  uint32_t r;
+  asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0"
+      : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ uint32_t byte1_x4(uint32_t x)
+{
+  uint32_t r;
+  asm("v_lshlrev_b32_sdwa %0, 2, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1"
+      : "=v"(r) : "v"(x));
+  return r;
+}
+__device__ __forceinline__ uint32_t ubfe(uint32_t x, uint32_t off, uint32_t w) { return __builtin_amdgcn_ubfe(x, off, w); }
+#else
+#ifdef __HIP__
+// hipcc's host pass parses the device code but never runs it
+#define ZFP_LDS_FN __device__ inline
+static constexpr char* zfp_emu_lds_base = nullptr;
+#else
+#define ZFP_LDS_FN inline
+inline char* zfp_emu_lds_base = nullptr;
+#endif
+typedef uint32_t lds_dword;
+ZFP_LDS_FN lds_dword* lds_at(uint32_t byte) { return (lds_dword*)(zfp_emu_lds_base + byte); }
+ZFP_LDS_FN uint32_t lds_off(const void* p) { return (uint32_t)((const char*)p - zfp_emu_lds_base); }
+ZFP_LDS_FN uint32_t byte0_x4(uint32_t x) { return (x & 0xffu) << 2; }
+ZFP_LDS_FN uint32_t byte1_x4(uint32_t x) { return ((x >> 8) & 0xffu) << 2; }
+ZFP_LDS_FN uint32_t ubfe(uint32_t x, uint32_t off, uint32_t w)
+{
+  off &= 31;
+  w &= 31;
+  return w ? (uint32_t)((x >> off) & ((1ull << w) - 1)) : 0u;
+}
+#undef ZFP_LDS_FN
+#endif
+
 // Scheduling fence (no instruction moves across it).
 #ifdef __HIP_DEVICE_COMPILE__
 #define ZFP_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
@@ -611,16 +689,19 @@ __device__ __forceinline__ uint32_t opaque_shr5(uint32_t x)
 
 // SIZE: coefficients per block (4^d; 64 for 3D).  Only the block's last
 // coefficient (implicit one and test) and the all-significant plane depend on it.
+// kstart, n0: start at plane kstart (wave-uniform) with n0 coefficients already
+// significant (the fixed-rate f32 coder hands over to this one mid-block).
 template <int PREC, bool PLIM, int SIZE = 64>
 __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, uint32_t pos, uint32_t lim,
                                                 uint32_t maxprec, const uint32_t (&Pl)[PREC],
-                                                const uint32_t (&Ph)[PREC])
+                                                const uint32_t (&Ph)[PREC], int kstart = PREC - 1, uint32_t n0 = 0)
 {
   const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
   uint32_t* const dm1 = s.d() - 1;  // dword j-1 of a position with j = ceil(p / 32)
   const uint32_t lim31 = lim + 31u;
   uint32_t p31 = pos + 31u;  // position + 31: j = p31 >> 5, alignbit shift = 31 - p31
-  uint32_t n = 0, nn = ~0u, Sl = 0, Sh = 0;
+  uint32_t n = n0, nn = ~n0;
+  uint32_t Sl = n0 >= 32u ? ~0u : (1u << n0) - 1u, Sh = n0 >= 64u ? ~0u : n0 > 32u ? (1u << (n0 - 32u)) - 1u : 0u;
   ExtEvent e0{0, 0, 0, 0}, e1{0, 0, 0, 0}, e2{0, 0, 0, 0};  // PREC > 32 only
 #ifdef ZFP_PLANE_UNROLL
 #pragma unroll ZFP_PLANE_UNROLL
@@ -628,6 +709,8 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
 #pragma unroll
 #endif
   for (int k = PREC - 1; k >= 0; k--) {
+    if (k > kstart)
+      continue;
     const bool act = p31 < lim31 && (!PLIM || (uint32_t)k >= kmin);
     // wave-level exit once every lane is done; without a precision limit
     // (fixed rate) only the low planes are checked: a block rarely spends
@@ -720,6 +803,94 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
   }
   const uint32_t end = p31 - 31u;
   return end < lim ? end : lim;
+}
+
+// ---------------------------------------------------------------------------
+// Fixed-rate coder of a 32-plane block (f32, encode3_aligned): the same planes
+// and bits as code_planes<32, false>, with a 32-bit plane body for the planes
+// in which no lane of the wave has anything in coefficients 32..63 and fewer
+// than 32 significant coefficients -- on smooth data all but the last few
+// planes (the C2 field: planes 31..8).  There the plane needs no 64-bit
+// arithmetic:
+//   xs = plane >> n (the not-yet-significant coefficients), bl = bitlen(xs),
+//   c = popcount(xs); the plane is n verbatim bits then e1 + 1 group bits with
+//   e1 = bl + c, g = (dbl(xs) << 1 | 1) - 2^e1 (code_planes' closed form: the
+//   leading test, the doubled-ones expansion, the top pair's surplus; xs == 0
+//   gives the single "0").  The first byte's expansion with the leading 1 and
+//   the shift for the second byte come from one table entry (lead[]).
+//   xs >= 0xffff (the top one past unit 0, or e1 == 32) takes the wave-uniform
+//   extension branch of code_planes.
+// The lane's position is kept as Q = -(bit address in LDS): the dword address
+// of a write is ~((Q >> 3) | 3) and the funnel shift is Q itself (mod 32).  At
+// the first plane where some lane leaves the 32-bit form (the condition only
+// becomes true once: n never shrinks) the rest of the block goes to
+// code_planes from that plane on.  `slot`: the lane's zeroed slot of `jmax`+1
+// dwords; lut: dbl[256] then lead[256] (CoderTables layout, in LDS).
+__device__ __forceinline__ void fr_write32(int32_t Q, uint32_t v)
+{
+  const uint32_t a = ~(((uint32_t)(Q >> 3)) | 3u);
+  __hip_atomic_fetch_or(lds_at(a), __builtin_amdgcn_alignbit(v, 0u, (uint32_t)Q), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+  __hip_atomic_fetch_or(lds_at(a + 4u), __builtin_amdgcn_alignbit(0u, v, (uint32_t)Q), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
+#ifndef ZFP_FR32
+#define ZFP_FR32 1
+#endif
+__device__ __forceinline__ void code_planes_fr32(uint32_t* slot, uint32_t jmax, const uint32_t* lut, uint32_t pos,
+                                                 uint32_t lim, const uint32_t (&Pl)[32], const uint32_t (&Ph)[32])
+{
+  OrSlot os{reinterpret_cast<uint64_t*>(slot), jmax};
+#if ZFP_FR32
+  const uint32_t sb = lds_off(slot) * 8u;  // slot bit address
+  const uint32_t tdbl = lds_off(lut), tlead = tdbl + 1024u;
+  int32_t Q = -(int32_t)(sb + pos);
+  const int32_t Qlim = -(int32_t)(sb + lim);
+  uint32_t n = 0;
+  bool m32 = true;
+  int ksw = 0;
+#pragma unroll
+  for (int k = 31; k >= 0; k--) {
+    if (m32) {
+      if (__builtin_amdgcn_ballot_w64(Ph[k] != 0u || n > 31u) != 0) {
+        m32 = false;
+        ksw = k;
+      } else {
+        const uint32_t pl = Pl[k];
+        const uint32_t xs = pl >> n;
+        const uint32_t l0 = *lds_at(tlead + byte0_x4(xs));
+        const uint32_t l1 = *lds_at(tdbl + byte1_x4(xs));
+        const uint32_t bl = 32u - (uint32_t)__clz((int)xs);
+        const uint32_t e1 = (uint32_t)__popc(xs) + bl;
+        fr_write32(Q, ubfe(pl, 0u, n));  // the n verbatim bits
+        const int32_t Qg = Q - (int32_t)n;
+        const uint32_t d = (l1 << (l0 & 31u)) | (l0 >> 5);  // (dbl(xs & 0xffff) << 1 | 1) mod 2^32
+        uint32_t g = d - (1u << (e1 & 31u));
+        const bool ext = xs > 0xfffeu;
+        if (__builtin_amdgcn_ballot_w64(ext) != 0) {
+          // rare: the lanes whose top one lies past unit 0 (or xs == 0xffff,
+          // whose group bits are 33 long) have no surplus in unit 0; their
+          // later units are written as in code_planes (bit 32 of the group
+          // bits is the last bit of an all-ones unit 0's expansion)
+          const uint32_t h = 31u - (uint32_t)__clz((int)xs);
+          const uint32_t gp = (uint32_t)(-Qg) - sb;
+          const uint32_t g32 = (xs & 0xffffu) == 0xffffu ? 1u : 0u;
+          g = ext ? d : g;
+          expand_event(os, lut, ExtEvent{gp, xs, 0u, ext ? h | (g32 << 7) : 0u});
+        }
+        fr_write32(Qg, g);
+        const int32_t Qn = Qg - (int32_t)e1 - 1;
+        Q = Qn > Qlim ? Qn : Qlim;
+        n += bl;
+      }
+    }
+  }
+  if (!m32)
+    code_planes<32, false>(os, lut, (uint32_t)(-Q) - sb, lim, 32u, Pl, Ph, ksw, n);
+#else
+  code_planes<32, false>(os, lut, pos, lim, 32u, Pl, Ph);
+#endif
 }
 
 // Decoder twin (decode.c:69-246), including the reference quirk that a

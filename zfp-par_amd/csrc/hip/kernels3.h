@@ -83,40 +83,49 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m
 // blocks form one contiguous run of words; with a stream offset r0 = g0
 // (mod 64) != 0 every output word is a funnel shift of two run words, and the
 // run's first and last words (shared with neighbouring waves) go to the
-// fix-up kernels.  Slots are swp >= slot_words_for(64 sw) words; words from sw
-// on are spare (bits past the budget) and never copied.
+// fix-up kernels.  Lane slots are sdw dwords apart (odd: the 32 lanes of a
+// ds_or_b32 half-wave at the same slot offset hit 32 different banks),
+// sdw >= slot_dwords_for(64 sw); dwords from 2 sw on are spare (bits past the
+// budget) and never copied.  magic_w / magic_c: ceil(2^32 / d) for d = sw and
+// d = sw / 2 (0 for d = 1).
+__host__ __device__ constexpr uint32_t slot_dwords_for(uint32_t lim) { return (lim + 95u) / 32u + 1u; }
+
 template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
-                                                       uint64_t* __restrict__ out, uint32_t sw, uint32_t swp,
-                                                       uint32_t magic, uint32_t r0, Partial* __restrict__ partials)
+                                                       uint64_t* __restrict__ out, uint32_t sw, uint32_t sdw,
+                                                       uint32_t magic_w, uint32_t magic_c, uint32_t r0,
+                                                       Partial* __restrict__ partials)
 {
-  __shared__ uint32_t lut[256];
-  extern __shared__ uint64_t lds[];
+  __shared__ uint32_t lut[512];  // CoderTables: dbl[256], lead[256]
+  extern __shared__ uint32_t ldsw[];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
-  uint64_t* wslot = lds + (size_t)wv * 64 * swp;
+  uint32_t* wslot = ldsw + (size_t)wv * 64 * sdw;
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
-#if ZFP_EARLY_GATHER
-  // the block loads are in flight while the wave fills its tables: every wave
-  // writes the whole (identical) table, so no workgroup barrier is needed
+  // the block loads are in flight while the wave copies the coder tables from
+  // device memory and zeroes its slots: every wave writes the whole (identical)
+  // tables, so no workgroup barrier is needed
   S v[64];
   BlockPos p{};
   if (b < g.nblocks) {
     p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
   }
-  encode_prologue_wave(lut, wslot, 64 * swp);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&kCoderTables);
+    uint4* dst = reinterpret_cast<uint4*>(lut);
+    dst[lane] = src[lane];
+    dst[lane + 64] = src[lane + 64];
+    uint4* z = reinterpret_cast<uint4*>(wslot);
+    for (uint32_t i = lane; i < 16 * sdw; i += 64)
+      z[i] = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only (vmcnt/expcnt at max)
+    __builtin_amdgcn_wave_barrier();
+  }
   if (b < g.nblocks) {
-#else
-  encode_prologue(lut, wslot, 64 * swp);
-  if (b < g.nblocks) {
-    S v[64];
-    BlockPos p = block_pos(g, b, 3);
-    gather3<S, VEC>(v, data, g, p);
-#endif
-    OrSlot os{wslot + (size_t)lane * swp, 2 * swp - 1};
+    OrSlot os{reinterpret_cast<uint64_t*>(wslot + (size_t)lane * sdw), sdw - 1};
     encode_block3<S, REV, true>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
   }
   if (first >= g.nblocks)
@@ -127,36 +136,31 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
   const uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
   const uint32_t total = (uint32_t)nb * sw;  // run length in words
   uint64_t* dst = out + first * sw;
+  // word i of the wave's run
+  auto run_word = [&](uint32_t i) -> uint64_t {
+    const uint32_t l = div_magic(i, magic_w);
+    const uint32_t* s = wslot + (size_t)l * sdw + 2 * (i - l * sw);
+    return (uint64_t)s[0] | ((uint64_t)s[1] << 32);
+  };
   if (r0 == 0) {
     if ((sw & 1) == 0) {
-      // 16-byte stores: word pairs never straddle two slots
-      for (uint32_t i = 2 * lane; i < total; i += 128) {
-        const uint32_t l = div_magic(i, magic);
-        const uint64_t* src = wslot + (size_t)l * swp + (i - l * sw);
-        ulonglong2 q;
-        q.x = src[0];
-        q.y = src[1];
-        *reinterpret_cast<ulonglong2*>(dst + i) = q;
+      // 16-byte stores: dword quads never straddle two slots
+      const uint32_t hw = sw >> 1, chunks = (uint32_t)nb * hw;
+      for (uint32_t c = lane; c < chunks; c += 64) {
+        const uint32_t l = div_magic(c, magic_c);
+        const uint32_t* s = wslot + (size_t)l * sdw + 4 * (c - l * hw);
+        *reinterpret_cast<uint4*>(dst + 2 * c) = make_uint4(s[0], s[1], s[2], s[3]);
       }
     } else {
-      for (uint32_t i = lane; i < total; i += 64) {
-        const uint32_t l = div_magic(i, magic);
-        dst[i] = wslot[(size_t)l * swp + (i - l * sw)];
-      }
+      for (uint32_t i = lane; i < total; i += 64)
+        dst[i] = run_word(i);
     }
     return;
   }
   // run words j = 0..total-1 land at bit r0 + 64 j of out[first*sw ...]
   for (uint32_t j = lane; j <= total; j += 64) {
-    uint64_t cur = 0, prev = 0;
-    if (j < total) {
-      const uint32_t l = div_magic(j, magic);
-      cur = wslot[(size_t)l * swp + (j - l * sw)];
-    }
-    if (j > 0) {
-      const uint32_t l = div_magic(j - 1, magic);
-      prev = wslot[(size_t)l * swp + (j - 1 - l * sw)];
-    }
+    const uint64_t cur = j < total ? run_word(j) : 0ull;
+    const uint64_t prev = j > 0 ? run_word(j - 1) : 0ull;
     const uint64_t val = (cur << r0) | (prev >> (64 - r0));
     if (j == 0) {
       partials[2 * w] = Partial{first * sw, val};

@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void scan_pass(ScanArgs a)
 // bitmap -> block index.  Tiles of kTileWords bitmap words per 256-thread group.
 constexpr uint32_t kTileWords = 2048;
 
-__global__ __launch_bounds__(256) void bm_tile_count(const uint64_t* __restrict__ bm, uint64_t nwords,
+static __global__ __launch_bounds__(256) void bm_tile_count(const uint64_t* __restrict__ bm, uint64_t nwords,
                                                      uint64_t* __restrict__ tile_cnt)
 {
   __shared__ uint32_t red[256];
@@ -372,7 +372,7 @@ __global__ __launch_bounds__(256) void bm_tile_count(const uint64_t* __restrict_
 }
 
 // exclusive scan of n tile counts in place (one 1024-thread group); total -> *sum
-__global__ __launch_bounds__(1024) void tile_scan(uint64_t* __restrict__ v, uint64_t n, uint64_t* __restrict__ sum)
+static __global__ __launch_bounds__(1024) void tile_scan(uint64_t* __restrict__ v, uint64_t n, uint64_t* __restrict__ sum)
 {
   __shared__ uint64_t part[1024];
   const uint64_t per = (n + 1023) / 1024;
@@ -399,7 +399,7 @@ __global__ __launch_bounds__(1024) void tile_scan(uint64_t* __restrict__ v, uint
 }
 
 // Set bit r of the bitmap with rank k (0-based) gives pos[k] = r, for k <= nb.
-__global__ __launch_bounds__(256) void bm_tile_emit(const uint64_t* __restrict__ bm, uint64_t nwords,
+static __global__ __launch_bounds__(256) void bm_tile_emit(const uint64_t* __restrict__ bm, uint64_t nwords,
                                                     const uint64_t* __restrict__ tile_off, uint64_t nb,
                                                     uint64_t* __restrict__ pos)
 {
@@ -438,7 +438,7 @@ __global__ __launch_bounds__(256) void bm_tile_emit(const uint64_t* __restrict__
 }
 
 // decoder index: per-block lengths and per-wave (nbw blocks) start offsets
-__global__ __launch_bounds__(256) void index_from_pos(const uint64_t* __restrict__ pos, uint64_t nb, uint32_t nbw,
+static __global__ __launch_bounds__(256) void index_from_pos(const uint64_t* __restrict__ pos, uint64_t nb, uint32_t nbw,
                                                       uint16_t* __restrict__ len, uint64_t* __restrict__ base)
 {
   const uint64_t b = (uint64_t)blockIdx.x * 256 + threadIdx.x;

@@ -25,9 +25,8 @@
 #include <thread>
 #include <vector>
 
-#include "kernels4.h"
 #include "kernels_n.h"
-#include "scan.h"
+#include "launch.h"
 #include "zfp_hip.h"
 
 using namespace zfp_amd;
@@ -389,20 +388,13 @@ static void launch_general3(Ctx* c, const Plan& p, const S* d_field, dim3 grid, 
   } else {
     if (p.dims == 1) return launch_enc_generic<S, 1>(c, p, d_field, grid, block, lds, a);
     if (p.dims == 2) return launch_enc_generic<S, 2>(c, p, d_field, grid, block, lds, a);
-    const bool rev = p.cp.minexp < kMinExp;
-    if (p.vec && rev)
-      hipLaunchKernelGGL((encode3_general<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else if (p.vec)
-      hipLaunchKernelGGL((encode3_general<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else if (rev)
-      hipLaunchKernelGGL((encode3_general<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else
-      hipLaunchKernelGGL((encode3_general<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    launch_encode3_general(Launch{grid, block, lds, c->stream}, p.vec, p.cp.minexp < kMinExp, HI, d_field, p.g,
+                           p.cp, a);
   }
 }
 
 template <typename S, bool HI>
-static void launch_decode3(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 block, size_t lds, const DecodeArgs& a)
+static void run_decode3(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 block, size_t lds, const DecodeArgs& a)
 {
   if constexpr (kIntField<S>) {
     if (p.dims == 1) launch_dec_generic<S, 1>(c, p, d_field, grid, block, lds, a);
@@ -411,24 +403,9 @@ static void launch_decode3(Ctx* c, const Plan& p, S* d_field, dim3 grid, dim3 bl
   } else {
     if (p.dims == 1) return launch_dec_generic<S, 1>(c, p, d_field, grid, block, lds, a);
     if (p.dims == 2) return launch_dec_generic<S, 2>(c, p, d_field, grid, block, lds, a);
-    const bool rev = p.cp.minexp < kMinExp;
-    if constexpr (HI) {
-      if (a.ovf) {  // short staging slots
-        if (p.vec)
-          hipLaunchKernelGGL((decode3<S, true, false, true, 3, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-        else
-          hipLaunchKernelGGL((decode3<S, false, false, true, 3, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-        return;
-      }
-    }
-    if (p.vec && rev)
-      hipLaunchKernelGGL((decode3<S, true, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else if (p.vec)
-      hipLaunchKernelGGL((decode3<S, true, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else if (rev)
-      hipLaunchKernelGGL((decode3<S, false, true, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else
-      hipLaunchKernelGGL((decode3<S, false, false, HI>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+    // short staging slots (a.ovf) exist for the f64 planes-32..63 decoder only
+    launch_decode3(Launch{grid, block, lds, c->stream}, p.vec, p.cp.minexp < kMinExp, HI, HI && a.ovf != nullptr,
+                   d_field, p.g, p.cp, a);
   }
 }
 
@@ -560,24 +537,13 @@ static void launch_encode4_kernel(Ctx* c, const Plan& p, const S* d_field, dim3 
   if constexpr (kIntField<S>) {
     launch_encode4_int(p.type, rev, p.vec, c->stream, grid, dim3(64), lds, d_field, p.g, p.cp, a);
   } else {
-#define ZFP_ENC4(V, R)                                                                                      \
-  do {                                                                                                      \
-    if (half)                                                                                               \
-      hipLaunchKernelGGL((encode4<S, V, R, true>), grid, dim3(64), lds, c->stream, d_field, p.g, p.cp, a);  \
-    else                                                                                                    \
-      hipLaunchKernelGGL((encode4<S, V, R, false>), grid, dim3(64), lds, c->stream, d_field, p.g, p.cp, a); \
-  } while (0)
-    if (p.vec && rev) ZFP_ENC4(true, true);
-    else if (p.vec) ZFP_ENC4(true, false);
-    else if (rev) ZFP_ENC4(false, true);
-    else ZFP_ENC4(false, false);
-#undef ZFP_ENC4
+    launch_encode4(Launch{grid, dim3(64), lds, c->stream}, p.vec, rev, half, d_field, p.g, p.cp, a);
   }
 }
 
 // 4D: encode4 for every mode (one 64-thread workgroup per 16 blocks)
 template <typename S>
-static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out, uint32_t g0,
+static int run_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out, uint32_t g0,
                           const Head& head, zfp_hip_index* index, uint64_t* total_bits)
 {
   using Int = typename Traits<S>::Int;
@@ -626,15 +592,8 @@ static int launch_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_o
         const size_t plds = (size_t)kEnc4HeadWords * 8 + std::max<size_t>((size_t)kBlocks4PerWave * swp_full * 8, xfull);
         const dim3 pg((n + kBlocks4PerWave - 1) / kBlocks4PerWave), pb(64);
         const OvfEntry* list = (const OvfEntry*)a.ovf;
-        const bool rev = p.cp.minexp < kMinExp;
-        if (p.vec && rev)
-          hipLaunchKernelGGL((encode4_patch<S, true, true>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
-        else if (p.vec)
-          hipLaunchKernelGGL((encode4_patch<S, true, false>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
-        else if (rev)
-          hipLaunchKernelGGL((encode4_patch<S, false, true>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
-        else
-          hipLaunchKernelGGL((encode4_patch<S, false, false>), pg, pb, plds, c->stream, d_field, p.g, p.cp, d_out, list, n, swp_full);
+        launch_encode4_patch(Launch{pg, pb, plds, c->stream}, p.vec, p.cp.minexp < kMinExp, d_field, p.g, p.cp, d_out,
+                             list, n, swp_full);
         HIP_TRY(hipGetLastError());
         HIP_TRY(hipEventRecord(c->ev[2], c->stream));
       }
@@ -649,7 +608,7 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
                          const Head& head, zfp_hip_index* index, uint64_t* total_bits)
 {
   if (p.dims == 4)
-    return launch_encode4<S>(c, p, d_field, d_out, g0, head, index, total_bits);
+    return run_encode4<S>(c, p, d_field, d_out, g0, head, index, total_bits);
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   const uint64_t ngroups = (nwaves + kWavesPerGroup - 1) / kWavesPerGroup;
   if (ngroups > 0x7fffffffull)
@@ -660,10 +619,11 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
   if constexpr (!kIntField<S>)
   if (p.fixed && (p.cp.maxbits % 64) == 0 && p.cp.maxprec >= (p.dbl ? 64u : 32u) && p.dims == 3) {
     const uint32_t sw = p.cp.maxbits / 64;
-    const uint32_t swp = (uint32_t)slot_words_odd(p.cp.maxbits);  // words from sw on are spare
-    const uint32_t magic = sw > 1 ? (uint32_t)((0x100000000ull + sw - 1) / sw) : 0u;
-    size_t lds = (size_t)kWavesPerGroup * 64 * swp * 8;
-    if (lds + kLutBytes > 160 * 1024)
+    const uint32_t sdw = slot_dwords_for(p.cp.maxbits) | 1u;  // dwords from 2 sw on are spare
+    auto magic_of = [](uint32_t d) { return d > 1 ? (uint32_t)((0x100000000ull + d - 1) / d) : 0u; };
+    const uint32_t magic_w = magic_of(sw), magic_c = (sw & 1) ? 0u : magic_of(sw / 2);
+    size_t lds = (size_t)kWavesPerGroup * 64 * sdw * 4;
+    if (lds + 2 * kLutBytes > 160 * 1024)
       return fail("zfp_hip: block size %u bits too large for LDS", p.cp.maxbits);
     Partial* parts = nullptr;
     if (g0) {
@@ -672,12 +632,8 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
       parts = (Partial*)c->partials.p;
     }
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    if (p.vec)
-      hipLaunchKernelGGL((encode3_aligned<S, true, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, d_out,
-                         sw, swp, magic, g0, parts);
-    else
-      hipLaunchKernelGGL((encode3_aligned<S, false, false>), grid, block, lds, c->stream, d_field, p.g, p.cp, d_out,
-                         sw, swp, magic, g0, parts);
+    launch_encode3_aligned(Launch{grid, block, lds, c->stream}, p.vec, d_field, p.g, p.cp, d_out, sw, sdw, magic_w,
+                           magic_c, g0, parts);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (g0) {
@@ -733,7 +689,7 @@ static int launch_encode(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_ou
 }
 
 template <typename S>
-static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
+static int run_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, uint64_t in_words, uint32_t g0,
                           const zfp_hip_index* index)
 {
   using Int = typename Traits<S>::Int;
@@ -793,14 +749,8 @@ static int launch_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_i
     const bool rev = p.cp.minexp < kMinExp;
     if constexpr (kIntField<S>)
       launch_decode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
-    else if (p.vec && rev)
-      hipLaunchKernelGGL((decode4<S, true, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else if (p.vec)
-      hipLaunchKernelGGL((decode4<S, true, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
-    else if (rev)
-      hipLaunchKernelGGL((decode4<S, false, true, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
     else
-      hipLaunchKernelGGL((decode4<S, false, false, true>), grid, block, lds, c->stream, d_field, p.g, p.cp, a);
+      launch_decode4(Launch{grid, block, lds, c->stream}, p.vec, rev, d_field, p.g, p.cp, a);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     if (!a.packw)
@@ -841,7 +791,7 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
                          const zfp_hip_index* index)
 {
   if (p.dims == 4)
-    return launch_decode4<S>(c, p, d_field, d_in, in_words, g0, index);
+    return run_decode4<S>(c, p, d_field, d_in, in_words, g0, index);
   const uint64_t nwaves = (p.g.nblocks + 63) / 64;
   if (!p.fixed && index->nwaves != nwaves)
     return fail("zfp_hip: block index has %llu waves, the 3D layout needs %llu", (unsigned long long)index->nwaves,
@@ -885,11 +835,11 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     if constexpr (sizeof(S) == 8) {
       if (hi_planes<S>(p))
-        launch_decode3<S, true>(c, p, d_field, grid, block, lds, a);
+        run_decode3<S, true>(c, p, d_field, grid, block, lds, a);
       else
-        launch_decode3<S, false>(c, p, d_field, grid, block, lds, a);
+        run_decode3<S, false>(c, p, d_field, grid, block, lds, a);
     } else {
-      launch_decode3<S, false>(c, p, d_field, grid, block, lds, a);
+      run_decode3<S, false>(c, p, d_field, grid, block, lds, a);
     }
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
@@ -1035,31 +985,9 @@ static uint64_t scan_seg_bits(uint64_t limit)
   return (L + 63) & ~63ull;
 }
 
-template <typename S, int DIMS, bool REV>
-static void launch_scan_pass(Ctx* c, const ScanArgs& a)
-{
-  const unsigned grid = (unsigned)((a.nseg + 255) / 256);
-  hipLaunchKernelGGL((scan_pass<S, DIMS, REV>), dim3(grid), dim3(256), 0, c->stream, a);
-}
-
-template <typename S>
-static void launch_scan_typed(Ctx* c, const Plan& p, const ScanArgs& a)
-{
-  const bool rev = p.cp.minexp < kMinExp;
-  switch (p.dims) {
-    case 1: rev ? launch_scan_pass<S, 1, true>(c, a) : launch_scan_pass<S, 1, false>(c, a); break;
-    case 2: rev ? launch_scan_pass<S, 2, true>(c, a) : launch_scan_pass<S, 2, false>(c, a); break;
-    case 3: rev ? launch_scan_pass<S, 3, true>(c, a) : launch_scan_pass<S, 3, false>(c, a); break;
-    default: rev ? launch_scan_pass<S, 4, true>(c, a) : launch_scan_pass<S, 4, false>(c, a); break;
-  }
-}
-
 static void launch_scan_dispatch(Ctx* c, const Plan& p, const ScanArgs& a)
 {
-  by_type(p, [&](auto tag) {
-    launch_scan_typed<std::remove_pointer_t<decltype(tag)>>(c, p, a);
-    return 1;
-  });
+  launch_scan_pass(p.type, p.dims, p.cp.minexp < kMinExp, dim3((unsigned)((a.nseg + 255) / 256)), c->stream, a);
 }
 
 static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_words, uint32_t g0,

@@ -1,0 +1,7 @@
+// 4D float (f32) kernels: the launch.h launchers of this type (launch_impl.h), compiled apart
+// from the host shim and from the other types.
+#include "launch_impl.h"
+
+namespace zfp_amd {
+ZFP_DEFINE4(float)
+}  // namespace zfp_amd

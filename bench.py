@@ -6,10 +6,17 @@ Workloads (--workload):
                 (BASELINE.json configs[1]) through the drop-in C API, field and
                 stream already in HBM.  With N GPUs each rank compresses its own
                 1024^3 z-slab chunk of an N*1024-plane field (weak scaling).
+  c3            one step = zfp_compress of a 1024^3 float64 field at fixed
+                precision 32 (configs[2]): variable-rate blocks, decoupled
+                look-back, block index; per rank its own 1024^3 z-slab.
   c4            one step = the zfpy chunk stream of configs[3]: per rank one
                 4096x4096x64 float32 z-slab of the 4096x4096x512 field, rate 8,
                 written after the 96-bit whole-field header exactly as
                 compress_numpy_portion lays it out (python/zfpy_c.pyx:330-376).
+  c5            one step = zfp_compress in reversible (lossless) mode of one
+                512x512x512x64 float32 w-slab of the 512^4 field of configs[4]
+                (4D blocks); rank r owns slab r (8 ranks = the whole field).
+                The lossless round trip is checked on the device.
 Chunks are independent zfp streams, so the timed region has no collective; the
 RCCL gather that concatenates the chunk streams on rank 0 is timed separately
 and reported as `gather`, never inside `value`.
@@ -58,7 +65,7 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--workload", choices=("c2", "c4"), default="c2")
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2")
     ap.add_argument("--n", type=int, default=N, help="c2: edge of the per-GPU cube (default 1024)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo plumbing check, no GPU")
@@ -78,16 +85,33 @@ def relaunch(args):
     return subprocess.call(cmd, env=env)
 
 
-def smooth_slab_torch(torch, nx, ny, nz, z0, device):
+def smooth_slab_torch(torch, nx, ny, nz, z0, device, dtype=None):
     """F1: v = sin(.05x) cos(.03y) + .5 sin(.02z + .01 x y / nx), x fastest, planes z0.."""
+    dtype = dtype or torch.float32
     x = torch.arange(nx, device=device, dtype=torch.float64)
     y = torch.arange(ny, device=device, dtype=torch.float64)
-    out = torch.empty((nz, ny, nx), device=device, dtype=torch.float32)
+    out = torch.empty((nz, ny, nx), device=device, dtype=dtype)
     base = (torch.sin(0.05 * x)[None, :] * torch.cos(0.03 * y)[:, None])
     xy = 0.01 * x[None, :] * y[:, None] / nx
     for k in range(nz):
         z = float(z0 + k)
-        out[k] = (base + 0.5 * torch.sin(0.02 * z + xy)).to(torch.float32)
+        out[k] = (base + 0.5 * torch.sin(0.02 * z + xy)).to(dtype)
+    return out
+
+
+def smooth_4d_torch(torch, n, nw, w0, device):
+    """F1 with the C5 w term: F1(x, y, z) + .25 cos(.04 w) for w = w0 .. w0 + nw - 1,
+    computed in float64 and rounded once (as tools/kprof.py field4)."""
+    import math
+    x = torch.arange(n, device=device, dtype=torch.float64)
+    base = torch.sin(0.05 * x)[None, :] * torch.cos(0.03 * x)[:, None]
+    xy = 0.01 * x[None, :] * x[:, None] / n
+    z = x[:, None, None]
+    f3 = base[None] + 0.5 * torch.sin(0.02 * z + xy[None])
+    out = torch.empty((nw, n, n, n), device=device, dtype=torch.float32)
+    for w in range(nw):
+        out[w] = (f3 + 0.25 * math.cos(0.04 * (w0 + w))).to(torch.float32)
+    del f3
     return out
 
 
@@ -130,8 +154,8 @@ def host_cores():
     return min(aff, quota) if quota else aff, aff, quota, model
 
 
-def cpu_baseline(field_np, rate, threads):
-    """The reference library (OpenMP policy) on the whole field; returns (GB/s, stream bytes, best s)."""
+def cpu_baseline(field_np, mode, param, threads):
+    """The reference library (OpenMP policy) compressing `field_np` in `mode`; returns (GB/s, stream bytes, best s)."""
     from pyoracle import REF_SO
     if not os.path.exists(REF_SO):
         return None
@@ -140,7 +164,7 @@ def cpu_baseline(field_np, rate, threads):
     ref.lib.zfp_stream_set_omp_threads.argtypes = [ctypes.c_void_p, ctypes.c_uint]
     f = ref.field_for(field_np)
     zs = ref.lib.zfp_stream_open(None)
-    ref.lib.zfp_stream_set_rate(zs, float(rate), 3, 3, 0)
+    ref.set_mode(zs, mode, param, 3 if field_np.dtype == np.float32 else 4, field_np.ndim)
     ref.lib.zfp_stream_set_omp_threads(zs, threads)
     cap = ref.lib.zfp_stream_maximum_size(zs, f)
     buf = np.zeros(cap, dtype=np.uint8)
@@ -158,6 +182,20 @@ def cpu_baseline(field_np, rate, threads):
     ref.lib.zfp_stream_close(zs)
     ref.lib.zfp_field_free(f)
     return field_np.nbytes / best / 1e9, buf[:nbytes], best
+
+
+# per workload: BASELINE config, dims, scalar, mode, dominant kernel, CPU-baseline sample (leading slab)
+WORKLOADS = {
+    "c2": dict(metric=METRIC, cfg="configs[1]", dtype="f32", mode="rate", param=16, kernel="encode3_aligned<float>",
+               sample_planes=None),
+    "c3": dict(metric="GB/s uncompressed, 3D float64 fixed-precision-32 encode, device-resident", cfg="configs[2]",
+               dtype="f64", mode="precision", param=32, kernel="encode3_general<double, hi planes>",
+               sample_planes=256),
+    "c4": dict(metric=METRIC, cfg="configs[3]", dtype="f32", mode="rate", param=8, kernel="encode3_aligned<float>",
+               sample_planes=None),
+    "c5": dict(metric="GB/s uncompressed, 4D float32 reversible (lossless) encode, device-resident", cfg="configs[4]",
+               dtype="f32", mode="reversible", param=None, kernel="encode4<float, reversible>", sample_planes=4),
+}
 
 
 def main():
@@ -187,30 +225,50 @@ def main():
     lib = api.lib
     lib.zfp_hip_last_timing.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 
-    if args.workload == "c2":
+    wl = WORKLOADS[args.workload]
+    f64 = wl["dtype"] == "f64"
+    tdtype = torch.float64 if f64 else torch.float32
+    es = 8 if f64 else 4
+    ztype = 4 if f64 else 3
+    hdr_field = None
+    if args.workload in ("c2", "c3"):
         n = args.n
-        nx, ny, nz, rate = n, n, n, 16
-        z0, ztot = rank * n, world * n
-        workload = "%d^3 float32 fixed-rate %d zfp_compress per GPU (BASELINE configs[1])" % (n, rate)
-    else:
-        nx, ny, nz, rate = 4096, 4096, 64, 8
-        z0, ztot = rank * 64, 512
+        shape = (n, n, n)  # numpy order: z, y, x
+        field_t = smooth_slab_torch(torch, n, n, n, rank * n, dev, tdtype)
+        workload = "%d^3 %s %s zfp_compress per GPU (BASELINE %s)" % (
+            n, "float64" if f64 else "float32",
+            "fixed-rate %g" % wl["param"] if wl["mode"] == "rate" else "fixed-precision %d" % wl["param"], wl["cfg"])
+        parallelism = "%d independent z-slab chunks, one per GPU" % world
+    elif args.workload == "c4":
+        shape = (64, 4096, 4096)
+        field_t = smooth_slab_torch(torch, 4096, 4096, 64, rank * 64, dev)
         workload = ("4096x4096x64 float32 fixed-rate 8 z-slab per GPU = one zfpy chunk of 4096x4096x512 "
                     "(BASELINE configs[3]), stream after the 96-bit whole-field header")
-    field_t = smooth_slab_torch(torch, nx, ny, nz, z0, dev)
+        parallelism = "%d independent z-slab chunks, one per GPU" % world
+    else:
+        n4 = 512 if args.n == N else args.n
+        nw = 64 if args.n == N else max(1, args.n // 8)
+        shape = (nw, n4, n4, n4)
+        field_t = smooth_4d_torch(torch, n4, nw, rank * nw, dev)
+        workload = ("%dx%dx%dx%d float32 reversible w-slab per GPU = chunk %d of the %d^4 field of BASELINE "
+                    "configs[4] (4D blocks)" % (n4, n4, n4, nw, rank, n4))
+        parallelism = "%d independent w-slab chunks, one per GPU" % world
     nvals = field_t.numel()
-    zf = lib.zfp_field_3d(ctypes.c_void_p(field_t.data_ptr()), 3, nx, ny, nz)
+    dims = len(shape)
+    ext = list(reversed(shape))
+    ptr = ctypes.c_void_p(field_t.data_ptr())
+    zf = lib.zfp_field_3d(ptr, ztype, *ext) if dims == 3 else lib.zfp_field_4d(ptr, ztype, *ext)
     zs = lib.zfp_stream_open(None)
-    # zfpy passes zfp_type_none to set_rate (pyx:300-302); the C API bench passes float
-    lib.zfp_stream_set_rate(zs, float(rate), 3 if args.workload == "c2" else 0, 3, 0)
+    if args.workload == "c4":
+        # zfpy passes zfp_type_none to set_rate (pyx:300-302); the C API bench passes the scalar type
+        lib.zfp_stream_set_rate(zs, 8.0, 0, 3, 0)
+        hdr_field = lib.zfp_field_3d(None, 3, 4096, 4096, 512)  # header of the whole field, in the device stream
+    else:
+        api.set_mode(zs, wl["mode"], wl["param"], ztype, dims)
     cap = lib.zfp_stream_maximum_size(zs, zf) + 64
     out_t = torch.zeros(cap, dtype=torch.uint8, device=dev)
     bs = lib.stream_open(ctypes.c_void_p(out_t.data_ptr()), cap)
     lib.zfp_stream_set_bit_stream(zs, bs)
-    hdr_field = None
-    if args.workload == "c4":
-        # header of the whole 4096x4096x512 field, written into the device stream
-        hdr_field = lib.zfp_field_3d(None, 3, nx, ny, ztot)
 
     def step():
         lib.zfp_stream_rewind(zs)
@@ -245,10 +303,11 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         ms = float(tt.item())
 
-    # decode of the same stream into a device buffer (reported, not the metric)
+    # decode of the same stream into a device buffer (reported, not the metric); variable-rate
+    # streams decode with the block index the compress call left on the stream
     back_t = torch.empty_like(field_t)
     lib.zfp_field_set_pointer(zf, ctypes.c_void_p(back_t.data_ptr()))
-    dms = []
+    dms, dkms = [], []
     for i in range(max(3, args.steps // 2)):
         lib.zfp_stream_rewind(zs)
         if hdr_field is not None:
@@ -260,11 +319,16 @@ def main():
         torch.cuda.synchronize()
         if i:
             dms.append((time.perf_counter() - t1) * 1e3)
+            k, t = ctypes.c_double(), ctypes.c_double()
+            lib.zfp_hip_last_timing(ctypes.byref(k), ctypes.byref(t))
+            dkms.append(k.value)
     lib.zfp_field_set_pointer(zf, ctypes.c_void_p(field_t.data_ptr()))
-    roundtrip_ok = None
-    if args.workload == "c2":
-        # fixed rate 16 is lossy: report the max error of the round trip
-        roundtrip_ok = float((back_t - field_t).abs().max().item())
+    roundtrip = {}
+    if wl["mode"] == "reversible":
+        roundtrip["lossless_roundtrip"] = bool(torch.equal(back_t, field_t))
+    else:
+        roundtrip["decode_max_abs_err"] = float((back_t - field_t).abs().max().item())
+    del back_t
 
     # gather of the chunk streams to rank 0 over RCCL (timed separately)
     gather = None
@@ -290,40 +354,49 @@ def main():
 
     if rank == 0:
         kernel_ms = float(np.mean(kms))
-        alg_bytes = nvals * 4 + nvals * rate // 8
+        # algorithmic bytes of the dominant kernel: the field read once, the stream written once
+        stream_bytes = nvals * wl["param"] // 8 if wl["mode"] == "rate" else int(nbytes)
+        alg_bytes = nvals * es + stream_bytes
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
         traffic, tsrc = traffic_from_profiles() if args.workload == "c2" else (None, None)
-        value = world * nvals * 4 / (ms * 1e-3) / 1e9
+        value = world * nvals * es / (ms * 1e-3) / 1e9
         result = {
-            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+            "metric": wl["metric"], "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "f32", "data": "synthetic (F1 smooth field generated on device)",
-            "config": {"workload": workload, "field_per_gpu": [nx, ny, nz], "rate": rate,
-                       "stream_bytes_per_gpu": int(nbytes),
-                       "parallelism": "%d independent z-slab chunks, one per GPU" % world},
+            "vs_baseline": None, "dtype": wl["dtype"], "data": "synthetic (F1 smooth field generated on device)",
+            "config": {"workload": workload, "field_per_gpu": ext, "mode": wl["mode"], "param": wl["param"],
+                       "stream_bytes_per_gpu": int(nbytes), "parallelism": parallelism},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "encode3_aligned<float>", "kernel_ms": round(kernel_ms, 4),
+                         "kernel": wl["kernel"], "kernel_ms": round(kernel_ms, 4),
                          "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": tsrc},
             "call_ms": round(float(np.mean(tms)), 4),
             "decode_ms": round(float(np.mean(dms)), 4) if dms else None,
-            "decode_GBps": round(nvals * 4 / (np.mean(dms) * 1e-3) / 1e9, 2) if dms else None,
-            "decode_max_abs_err": roundtrip_ok,
+            "decode_kernel_ms": round(float(np.mean(dkms)), 4) if dkms else None,
+            "decode_GBps": round(nvals * es / (np.mean(dms) * 1e-3) / 1e9, 2) if dms else None,
             "gather": gather,
         }
-        if not args.no_cpu and world == 1 and args.workload == "c2":
+        result.update(roundtrip)
+        if not args.no_cpu and world == 1 and args.workload != "c4":
             cores, aff, quota, model = host_cores()
-            sample = field_t.cpu().numpy()
-            cb = cpu_baseline(sample, rate, cores)
+            planes = wl["sample_planes"]
+            sample_t = field_t if planes is None else field_t[:planes]
+            sample = sample_t.cpu().numpy()
+            cb = cpu_baseline(sample, wl["mode"], wl["param"], cores)
             if cb is not None:
                 gbs, ref_bytes, best = cb
-                gpu_bytes = out_t[: len(ref_bytes)].cpu().numpy()
+                what = ("the full %s field" % "x".join(map(str, ext)) if planes is None else
+                        "the leading %s slab of the per-GPU field" % "x".join(map(str, list(reversed(sample.shape)))))
                 result["cpu_baseline"] = {
                     "value": round(gbs, 3), "unit": "GB/s", "cores": cores, "kind": "reference",
-                    "sample": "the full %dx%dx%d field, reference zfp_compress exec=omp with %d threads, best of 3 "
-                              "(%.3f s)" % (nx, ny, nz, cores, best),
+                    "sample": "%s, reference zfp_compress exec=omp with %d threads, best of 3 (%.3f s)" % (
+                        what, cores, best),
                     "cpu_model": model, "affinity_cpus": aff, "cgroup_cpu_quota": quota}
-                result["bitexact_vs_reference"] = bool(np.array_equal(gpu_bytes, ref_bytes))
+                # the sample is a leading slab: its stream is a prefix of the GPU stream (blocks in
+                # raster order); the last word also holds the next blocks' bits on the GPU side
+                nw_cmp = len(ref_bytes) // 8 - (0 if planes is None else 1)
+                gpu_bytes = out_t[: nw_cmp * 8].cpu().numpy()
+                result["bitexact_vs_reference"] = bool(np.array_equal(gpu_bytes, ref_bytes[: nw_cmp * 8]))
             else:
                 result["cpu_baseline"] = None
         print(json.dumps(result), flush=True)
@@ -362,7 +435,8 @@ def dry_run(args, torch, dist, world, rank):
                           "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 4),
                           "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
                           "data": "synthetic", "dry_run": True,
-                          "config": {"workload": "dry run: numpy copy of 4 MiB per rank (no codec, no GPU)"}}),
+                          "config": {"workload": "dry run of --workload %s: numpy copy of 4 MiB per rank "
+                                                 "(no codec, no GPU)" % args.workload}}),
               flush=True)
     if distributed:
         dist.destroy_process_group()

@@ -114,7 +114,8 @@ static int run_fr32(std::mt19937_64& rng, int trials)
         case 6: lo = (k > 24) ? (1ull << (rng() % 32)) : (r & (r >> 5) & 0xffffffffull); break;
         default: lo = (rng() % 2) ? 0xffff0000ull | (r & 0xffff) : ((r & 0xffff) << 16); break;  // tops past bit 15
       }
-      P[k] = k >= khi ? lo : (lo | (r & 0xffffffff00000000ull));
+      const uint64_t hi = (t & 8) ? ((rng() % 3 == 0) ? (1ull << (32 + rng() % 3)) : 0ull) : (r & 0xffffffff00000000ull);
+      P[k] = k >= khi ? lo : (lo | hi);
     }
     uint32_t Pl[32], Ph[32];
     for (int k = 0; k < 32; k++) Pl[k] = (uint32_t)P[k], Ph[k] = (uint32_t)(P[k] >> 32);
@@ -139,6 +140,65 @@ static int run_fr32(std::mt19937_64& rng, int trials)
   return bad;
 }
 
+// The 32-plane decoder (decode_planes32) on streams written by the reference
+// coder loop: the same plane patterns as run_fr32, budgets cut anywhere and
+// precision limits; planes and consumed bits must match.
+static int run_dec32(std::mt19937_64& rng, int trials)
+{
+  uint32_t sq[256];
+  for (int b = 0; b < 256; b++) sq[b] = squeeze_entry(b);
+  int bad = 0;
+  for (int t = 0; t < trials; t++) {
+    uint64_t P[32];
+    const int kind = t % 8;
+    const int khi = (int)(rng() % 33);
+    for (int k = 0; k < 32; k++) {
+      uint64_t r = rng();
+      uint64_t lo;
+      switch (kind) {
+        case 0: lo = r & 0xffffffffull; break;
+        case 1: lo = (rng() % 3 == 0) ? r & rng() & 0xffffffffull : 0; break;
+        case 2: lo = (rng() % 4 == 0) ? 0xffffull << (rng() % 17) : (r & 0xffff); break;
+        case 3: lo = (rng() % 5 == 0) ? (1ull << 31) : (r & 0xff); break;
+        case 4: lo = (k % 7 == 0) ? 0xffffffffull : 0; break;
+        case 5: lo = (r & 0xffffffffull) >> (rng() % 32); break;
+        case 6: lo = (k > 24) ? (1ull << (rng() % 32)) : (r & (r >> 5) & 0xffffffffull); break;
+        default: lo = (rng() % 2) ? 0xffff0000ull | (r & 0xffff) : ((r & 0xffff) << 16); break;
+      }
+      // high half: dense, or only coefficients 32..34 (sections ending right at the 32-bit edge)
+      const uint64_t hi = (t & 8) ? ((rng() % 3 == 0) ? (1ull << (32 + rng() % 3)) : 0ull) : (r & 0xffffffff00000000ull);
+      if (t & 16)
+        lo &= (1ull << (rng() % 33)) - 1 | (1ull << 31);
+      P[k] = k >= khi ? lo : (lo | hi);
+    }
+    const uint32_t budgets[3] = {4096, 64 + (uint32_t)(rng() % 1500), 1 + (uint32_t)(rng() % 300)};
+    for (uint32_t budget : budgets) {
+      const uint32_t maxprec = (t % 3 == 0) ? 1 + (uint32_t)(rng() % 32) : 64;
+      std::vector<uint64_t> w(200, 0);
+      const uint32_t len = ref_code(w, 0, budget, maxprec, P, 32);
+      // what the reference decoder reconstructs: the coded planes, bits past the cut zero
+      uint64_t want[32];
+      {
+        std::vector<uint64_t> w2(200, 0);
+        for (int k = 0; k < 32; k++) want[k] = 0;
+        // decode with the literal loop (decode_planes64 is itself checked against it in dec_emu)
+        WordReader r0{w.data(), 0};
+        decode_planes64<32>(r0, sq, budget, maxprec, want);
+      }
+      uint64_t got[32];
+      WordReader r{w.data(), 0};
+      const uint32_t used = decode_planes32(r, sq, budget, maxprec, got);
+      bool ok = used == len && r.pos == len;
+      for (int k = 0; ok && k < 32; k++) ok = got[k] == want[k];
+      if (!ok && bad++ < 5)
+        printf("dec32 trial %d kind %d khi %d budget %u maxprec %u: used %u vs %u\n", t, kind, khi, budget, maxprec, used,
+               len);
+    }
+  }
+  printf("dec32 mismatches %d\n", bad);
+  return bad;
+}
+
 int main()
 {
   std::mt19937_64 rng(12345);
@@ -146,6 +206,7 @@ int main()
   for (int all : {0, 1}) {
     emu_any_all = all;
     bad += run_fr32(rng, 40000);
+    bad += run_dec32(rng, 20000);
   }
   for (int all : {0, 1}) {  // 1: every wave-level branch entered (other lanes need it)
     emu_any_all = all;

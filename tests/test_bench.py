@@ -7,13 +7,16 @@ import os
 import subprocess
 import sys
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(gpus):
+def _run(gpus, workload="c2"):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", str(gpus), "--dry-run",
-                        "--steps", "3", "--warmup", "1"], capture_output=True, text=True, timeout=300, env=env)
+                        "--steps", "3", "--warmup", "1", "--workload", workload], capture_output=True, text=True,
+                       timeout=300, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -31,3 +34,9 @@ def test_launcher_spawns_two_ranks():
 def test_single_rank_runs_in_process():
     d = _run(1)
     assert d["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("workload", ["c3", "c5"])
+def test_variable_rate_workloads_launch_two_ranks(workload):
+    d = _run(2, workload)
+    assert d["n_gpus"] == 2 and workload in d["config"]["workload"]

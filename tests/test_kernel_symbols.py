@@ -1,0 +1,98 @@
+"""Every kernel the host code can launch has gfx950 device code (CPU test).
+
+A template kernel whose host launch stub is compiled but whose device code is
+not instantiated makes HIP abort the calling process at launch ("could not
+find the symbol"), breaking the C API's "return 0, stream untouched" contract.
+This test reads libzfp_hip.so without a GPU: the host stubs from its symbol
+table, the device kernels from the gfx950 code objects in its .hip_fatbin
+section (clang offload bundles of ELF code objects), and checks that every stub
+has a kernel descriptor (`<name>.kd`) in some code object.
+"""
+import os
+import re
+import struct
+import subprocess
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB = os.path.join(REPO, "zfp-par_amd", "lib", "libzfp_hip.so")
+MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+
+
+def _sections(elf):
+    """(name, type, offset, size, link) of every section of an ELF64 image."""
+    shoff, = struct.unpack_from("<Q", elf, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+    hdrs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + i * shentsize) for i in range(shnum)]
+    stro = hdrs[shstrndx][4]
+    out = []
+    for h in hdrs:
+        nm = elf[stro + h[0]: elf.index(b"\0", stro + h[0])].decode()
+        out.append((nm, h[1], h[4], h[5], h[6]))
+    return out
+
+
+def _symbols(elf):
+    secs = _sections(elf)
+    names = set()
+    for nm, typ, off, size, link in secs:
+        if typ not in (2, 11):  # SHT_SYMTAB, SHT_DYNSYM
+            continue
+        stro = secs[link][2]
+        for i in range(size // 24):
+            st_name, = struct.unpack_from("<I", elf, off + i * 24)
+            if st_name:
+                names.add(elf[stro + st_name: elf.index(b"\0", stro + st_name)].decode())
+    return names
+
+
+def _device_kernels(lib_bytes):
+    secs = {nm: (off, size) for nm, _, off, size, _ in _sections(lib_bytes)}
+    off, size = secs[".hip_fatbin"]
+    fb = lib_bytes[off: off + size]
+    kernels, objects, i = set(), 0, 0
+    while True:
+        j = fb.find(MAGIC, i)
+        if j < 0:
+            break
+        n, = struct.unpack_from("<Q", fb, j + 24)
+        p = j + 32
+        for _ in range(n):
+            o, sz, tl = struct.unpack_from("<QQQ", fb, p)
+            p += 24
+            triple = fb[p: p + tl].decode()
+            p += tl
+            if "gfx950" in triple and sz:
+                objects += 1
+                kernels |= {s[:-3] for s in _symbols(fb[j + o: j + o + sz]) if s.endswith(".kd")}
+        i = j + len(MAGIC)
+    return kernels, objects
+
+
+_STUB = re.compile(r"^(_Z(?:N7zfp_amd)?L?)(\d+)__device_stub__(.*)$")
+
+
+def _host_stub_kernels():
+    out = subprocess.run(["nm", LIB], capture_output=True, text=True, check=True).stdout
+    kernels = set()
+    for line in out.splitlines():
+        name = line.split()[-1]
+        m = _STUB.match(name)
+        if not m:
+            continue
+        n = int(m.group(2)) - len("__device_stub__")
+        rest = m.group(3)
+        kernels.add("%s%d%s" % (m.group(1), n, rest))
+    return kernels
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libzfp_hip.so not built")
+def test_every_host_kernel_stub_has_gfx950_code():
+    data = open(LIB, "rb").read()
+    device, objects = _device_kernels(data)
+    host = _host_stub_kernels()
+    assert objects >= 1, "no gfx950 code object in .hip_fatbin"
+    assert len(host) > 20, "host kernel stubs not found (%d)" % len(host)
+    missing = sorted(host - device)
+    assert not missing, "kernels launched by the host without device code:\n  " + "\n  ".join(missing[:20])

@@ -92,6 +92,25 @@ struct alignas(16) Vec16 {
   S v[N];
 };
 
+// Streaming field reads (each byte is read once): ZFP_NT_LOAD marks them
+// non-temporal.
+#ifndef ZFP_NT_LOAD
+#define ZFP_NT_LOAD 0
+#endif
+template <typename S, int N>
+__device__ __forceinline__ Vec16<S, N> load16(const S* p)
+{
+#if ZFP_NT_LOAD && defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  const u4 x = __builtin_nontemporal_load(reinterpret_cast<const u4*>(p));
+  Vec16<S, N> r;
+  __builtin_memcpy(&r, &x, 16);
+  return r;
+#else
+  return *reinterpret_cast<const Vec16<S, N>*>(p);
+#endif
+}
+
 template <typename S, bool VEC>
 __device__ __forceinline__ void gather3(S (&v)[64], const S* __restrict__ base, const Geometry& g, const BlockPos& p)
 {
@@ -106,13 +125,13 @@ __device__ __forceinline__ void gather3(S (&v)[64], const S* __restrict__ base, 
         if (VEC) {
           // 16-byte loads of any scalar type (4 floats/int32 or 2 doubles/int64)
           if constexpr (sizeof(S) == 4) {
-            const Vec16<S, 4> q = *reinterpret_cast<const Vec16<S, 4>*>(r);
+            const Vec16<S, 4> q = load16<S, 4>(r);
 #pragma unroll
             for (int i = 0; i < 4; i++)
               v[16 * k + 4 * j + i] = q.v[i];
           } else {
-            const Vec16<S, 2> q0 = *reinterpret_cast<const Vec16<S, 2>*>(r);
-            const Vec16<S, 2> q1 = *reinterpret_cast<const Vec16<S, 2>*>(r + 2);
+            const Vec16<S, 2> q0 = load16<S, 2>(r);
+            const Vec16<S, 2> q1 = load16<S, 2>(r + 2);
             v[16 * k + 4 * j + 0] = q0.v[0];
             v[16 * k + 4 * j + 1] = q0.v[1];
             v[16 * k + 4 * j + 2] = q1.v[0];
@@ -391,13 +410,17 @@ __device__ __forceinline__ uint32_t decode_ints3(WordReader& r, const uint32_t* 
   constexpr int PREC = Traits<S>::kIntPrec;
   if constexpr (HI && PREC == 64) {
     uint64_t P[32];
-    const uint32_t used = decode_planes64<32, false>(r, sq, budget, prec, P);
+    const uint32_t used = decode_planes32<false>(r, sq, budget, prec, P);
     pin_registers(P);
     coeffs_from_planes_hi(q, P);
     return used;
   } else {
     uint64_t P[PREC];
-    uint32_t used = decode_planes64<PREC>(r, sq, budget, prec, P);
+    uint32_t used;
+    if constexpr (PREC == 32)
+      used = decode_planes32(r, sq, budget, prec, P);
+    else
+      used = decode_planes64<PREC>(r, sq, budget, prec, P);
     pin_registers(P);
     if constexpr (PREC == 32)
       coeffs_from_planes(q, P);

@@ -1066,4 +1066,97 @@ __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_
   return budget - bits;
 }
 
+// ---------------------------------------------------------------------------
+// 32-plane decoder (f32 blocks) with a 32-bit plane body, the twin of
+// code_planes_fr32: while every lane of the wave has fewer than 32
+// significant coefficients, a plane is parsed from ONE 64-bit window at its
+// start (the n verbatim bits, the lead test and 31 section bits), with 32-bit
+// arithmetic: the section's end by decode_plane64's carry trick on 31 bits,
+// its ones squeezed out with the byte table.  A lane takes decode_plane64
+// (the reference loop included) for the plane instead when its section does
+// not end inside the window, makes coefficient 32 or later significant, or
+// its budget could end inside the plane (bits < 64); past its precision limit
+// a lane reads nothing.  Once some lane has 32 significant coefficients the
+// remaining planes go to decode_plane64 for every lane.
+#ifndef ZFP_DEC32
+#define ZFP_DEC32 1
+#endif
+template <bool IMP = true>
+__device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_t* sq, uint32_t budget,
+                                                    uint32_t maxprec, uint64_t (&P)[32])
+{
+#if !ZFP_DEC32
+  return decode_planes64<32, IMP>(r, sq, budget, maxprec, P);
+#else
+  const uint32_t kmin = 32u > maxprec ? 32u - maxprec : 0u;
+  uint32_t bits = budget, n = 0;
+#pragma unroll
+  for (int k = 0; k < 32; k++)
+    P[k] = 0;
+  bool m32 = true;
+  int ksw = -1;
+#pragma unroll
+  for (int k = 31; k >= 0; k--) {
+    if (!m32)
+      continue;
+    if (__builtin_amdgcn_ballot_w64(n > 31u) != 0) {
+      m32 = false;
+      ksw = k;
+      continue;
+    }
+    const bool act = bits != 0 && (uint32_t)k >= kmin;
+    if (__builtin_amdgcn_ballot_w64(act) == 0) {  // every lane done (budget or precision): so are later planes
+      m32 = false;
+      continue;
+    }
+    const uint64_t W = r.peek_at(r.pos);
+    const uint32_t lo = (uint32_t)W, hi = (uint32_t)(W >> 32);
+    const uint32_t g = __builtin_amdgcn_alignbit(hi, lo, n);  // stream bits n .. n+31 of the plane
+    const uint32_t S = g >> 1;                                // 31 section bits after the lead test
+    const uint32_t starts = S & ~(S << 1);
+    const uint32_t se = S + (starts & 0x55555555u), so = S + (starts & 0xaaaaaaaau);
+    // bit 31 of S is not data: a run reaching bit 30 has not ended there
+    const uint32_t ends = ((se & ~S) & 0x2aaaaaaau) | ((so & ~S) & 0x55555555u);
+    const uint32_t q = ends ? (uint32_t)__builtin_ctz(ends) : 32u;
+    const uint32_t mq = (ends - 1u) & ~ends;
+    const uint32_t ones = (uint32_t)__popc(S & mq);
+    const uint32_t np = q - (ones - 1u) / 2u;  // coefficient positions the section covers
+    const bool one = (g & 1u) != 0;
+    const bool fast = act && bits >= 64u && (!one || (ends != 0u && n + np <= 32u));
+    const uint32_t F = one ? S & mq & (((S & ~se) & 0x55555555u) | ((S & ~so) & 0xaaaaaaaau)) : 0u;
+    const uint32_t xx = squeeze32(sq, F);
+    const uint32_t x = ubfe(lo, 0u, n) | (xx << n);
+    const uint32_t used = n + (one ? q + 2u : 1u);
+    if (fast) {
+      P[k] = x;
+      r.pos += used;
+      bits -= used;
+      n += one ? np : 0u;
+    }
+    const bool slow = act && !fast;
+    if (__builtin_amdgcn_ballot_w64(slow) != 0) {
+      if (slow) {
+        uint32_t b = bits;
+        P[k] = decode_plane64<IMP>(r, sq, b, n);
+        bits = b;
+      }
+    }
+  }
+  if (!m32) {
+#pragma unroll
+    for (int k = 31; k >= 0; k--) {
+      if (k > ksw)
+        continue;
+      const bool act = bits != 0 && (uint32_t)k >= kmin;
+      if (__builtin_amdgcn_ballot_w64(act) == 0)
+        break;
+      uint32_t b = act ? bits : 0u;  // a lane past its precision limit decodes with no budget: no effect
+      P[k] = decode_plane64<IMP>(r, sq, b, n);
+      bits = act ? b : bits;
+    }
+  }
+  return budget - bits;
+#endif
+}
+
 }  // namespace zfp_amd

@@ -90,6 +90,18 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m
 // d = sw / 2 (0 for d = 1).
 __host__ __device__ constexpr uint32_t slot_dwords_for(uint32_t lim) { return (lim + 95u) / 32u + 1u; }
 
+// the stream is written once and not read back by this kernel
+#ifndef ZFP_NT_STORE
+#define ZFP_NT_STORE 0
+#endif
+// wave priority while issuing the field loads / the copy-out (0: unchanged)
+#ifndef ZFP_ENC_PRIO
+#define ZFP_ENC_PRIO 0
+#endif
+#ifndef ZFP_ENC_PRIO_OUT
+#define ZFP_ENC_PRIO_OUT 0
+#endif
+
 template <typename S, bool VEC, bool REV>
 __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        uint64_t* __restrict__ out, uint32_t sw, uint32_t sdw,
@@ -109,10 +121,16 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
   // tables, so no workgroup barrier is needed
   S v[64];
   BlockPos p{};
+#if ZFP_ENC_PRIO
+  __builtin_amdgcn_s_setprio(ZFP_ENC_PRIO);  // issue the loads ahead of the coding waves
+#endif
   if (b < g.nblocks) {
     p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
   }
+#if ZFP_ENC_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   {
     const uint4* src = reinterpret_cast<const uint4*>(&kCoderTables);
     uint4* dst = reinterpret_cast<uint4*>(lut);
@@ -133,6 +151,9 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
   // slots are read across lanes of this wave only: LDS ops of a wave complete in order
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+#if ZFP_ENC_PRIO_OUT
+  __builtin_amdgcn_s_setprio(ZFP_ENC_PRIO_OUT);
+#endif
   const uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
   const uint32_t total = (uint32_t)nb * sw;  // run length in words
   uint64_t* dst = out + first * sw;
@@ -149,7 +170,12 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
       for (uint32_t c = lane; c < chunks; c += 64) {
         const uint32_t l = div_magic(c, magic_c);
         const uint32_t* s = wslot + (size_t)l * sdw + 4 * (c - l * hw);
+#if ZFP_NT_STORE && defined(__HIP_DEVICE_COMPILE__)
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u4{s[0], s[1], s[2], s[3]}, reinterpret_cast<u4*>(dst + 2 * c));
+#else
         *reinterpret_cast<uint4*>(dst + 2 * c) = make_uint4(s[0], s[1], s[2], s[3]);
+#endif
       }
     } else {
       for (uint32_t i = lane; i < total; i += 64)

@@ -55,6 +55,10 @@ static int fail(const char* fmt, ...)
 
 // ---------------------------------------------------------------------------
 // block index (variable-rate streams)
+// An index describes one stream: it records the codec settings, the layout
+// and a fingerprint of the stream's words (stream_fingerprint), and is used
+// only for a stream that matches all of them (index_matches) -- another
+// stream of the same shape, a changed mode or a rewritten buffer is scanned.
 struct zfp_hip_index {
   int device = -1;
   uint64_t nblocks = 0;
@@ -62,6 +66,10 @@ struct zfp_hip_index {
   uint32_t per_wave = 0;       // blocks per wave of the layout it was made for (64: 3D, 16: 4D)
   uint64_t start_bit = ~0ull;  // stream bit offset of block 0 it was made for
   uint64_t total_bits = 0;
+  uint64_t fp = 0;             // stream_fingerprint of the stream it was made for
+  uint32_t minbits = 0, maxbits = 0, maxprec = 0;
+  int32_t minexp = 0;
+  int32_t type = 0, dims = 0;
   uint16_t* d_len = nullptr;   // per-block bit length
   uint64_t* d_base = nullptr;  // per-wave start bit relative to the stream's first block
   size_t cap_blocks = 0, cap_waves = 0;
@@ -97,6 +105,30 @@ static void index_release(zfp_hip_index* x)
   x->cap_blocks = x->cap_waves = 0;
   x->nblocks = x->nwaves = 0;
   x->start_bit = ~0ull;
+  x->fp = 0;
+}
+
+// Fingerprint of the stream bits [start_bit, start_bit + total_bits): a hash
+// of the bit count and of 16 words spread evenly over the range (the first
+// and last masked to the range).  Two streams of one field and mode whose
+// block lengths differ anywhere differ in the words after that block, so an
+// index is not used for a stream it does not describe (a stream that matches
+// in every sampled word and in length has, in practice, the same block
+// offsets).  Host streams are read in place; device streams through a small
+// gather kernel.
+constexpr int kFpWords = 16;
+
+static __global__ void fp_gather(const uint64_t* __restrict__ w, uint64_t W0, uint64_t n, uint64_t* __restrict__ out)
+{
+  const uint32_t i = threadIdx.x;
+  if (i < kFpWords)
+    out[i] = w[W0 + (n - 1) * i / (kFpWords - 1)];
+}
+
+static uint64_t fp_mix(uint64_t h, uint64_t v)
+{
+  h ^= v + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+  return h * 0xff51afd7ed558ccdull;
 }
 
 // ---------------------------------------------------------------------------
@@ -115,7 +147,7 @@ struct Ctx {
   hipStream_t stream = nullptr;
   hipStream_t side[2] = {nullptr, nullptr};  // host slab pipeline: uploads, downloads
   hipEvent_t ev[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};  // [4], [5]: index scan
-  Scratch field, words, status, partials, misc, ovf;
+  Scratch field, words, status, partials, misc, ovf, fpbuf;
   Scratch scan_bm, scan_seg, scan_tiles, scan_pos;  // index scan of a stream without index
   zfp_hip_index scan_index;                         // index built by the scan
 };
@@ -141,8 +173,8 @@ static void free_scratch(Scratch& s)
 static void destroy_ctx(Ctx* c)
 {
   (void)hipSetDevice(c->device);
-  for (Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->ovf, &c->scan_bm, &c->scan_seg,
-                     &c->scan_tiles, &c->scan_pos})
+  for (Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->ovf, &c->fpbuf, &c->scan_bm,
+                     &c->scan_seg, &c->scan_tiles, &c->scan_pos})
     free_scratch(*s);
   index_release(&c->scan_index);
   for (auto& e : c->ev)
@@ -236,6 +268,39 @@ static bool is_device_ptr(const void* p)
   return attr.type == hipMemoryTypeDevice;
 }
 
+static int stream_fingerprint(Ctx* c, const uint64_t* words, bool dev, uint64_t start_bit, uint64_t total_bits,
+                              uint64_t* fp)
+{
+  const uint64_t W0 = start_bit >> 6, end = start_bit + total_bits;
+  const uint64_t n = total_bits ? ((end + 63) >> 6) - W0 : 1;
+  uint64_t v[kFpWords];
+  if (dev) {
+    if (!ensure(c->fpbuf, kFpWords * 8))
+      return 0;
+    hipLaunchKernelGGL(fp_gather, dim3(1), dim3(64), 0, c->stream, words, W0, n, (uint64_t*)c->fpbuf.p);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(v, c->fpbuf.p, sizeof v, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  } else {
+    for (int i = 0; i < kFpWords; i++)
+      v[i] = words[W0 + (n - 1) * (uint64_t)i / (kFpWords - 1)];
+  }
+  uint64_t h = fp_mix(0x7a6670ull, total_bits);
+  for (int i = 0; i < kFpWords; i++) {
+    const uint64_t wi = W0 + (n - 1) * (uint64_t)i / (kFpWords - 1);
+    uint64_t m = ~0ull;
+    if (wi == W0)
+      m &= ~0ull << (start_bit & 63);
+    if (total_bits && wi == ((end - 1) >> 6) && (end & 63))
+      m &= (1ull << (end & 63)) - 1;
+    if (!total_bits)
+      m = 0;
+    h = fp_mix(h, v[i] & m);
+  }
+  *fp = h;
+  return 1;
+}
+
 // ---------------------------------------------------------------------------
 // job analysis
 struct Plan {
@@ -318,6 +383,17 @@ static int plan_job(const zfp_hip_job* j, const void* field_base, Plan& p)
   if (!p.fixed && p.max_len > 0xffff)
     return fail("zfp_hip: block length bound %u bits exceeds the block index (16-bit lengths)", p.max_len);
   return 1;
+}
+
+// the codec settings and layout an index is made for
+static void index_stamp(zfp_hip_index* x, const Plan& p)
+{
+  x->minbits = p.cp.minbits;
+  x->maxbits = p.cp.maxbits;
+  x->maxprec = p.cp.maxprec;
+  x->minexp = p.cp.minexp;
+  x->type = p.type;
+  x->dims = p.dims;
 }
 
 static size_t slot_words_odd(uint32_t bits)
@@ -934,21 +1010,33 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
   }
   if (g.s[0] != 1)
     return fail("zfp_hip: host-resident decompression of a non-slab chunk needs unit x stride");
-  // to host: the span through a private buffer, then exactly the box's rows
-  // (neighbouring boxes of the same array may be written concurrently)
+  // to host: the box's rows, (z, w) slice by slice, into a private dense
+  // buffer (2D copies), then row by row into the field (neighbouring boxes of
+  // the same array may be written concurrently, and the pageable copy path may
+  // write whole pages)
   if (to_host) {
-    const size_t off0 = (size_t)p.span_lo * es, span = (size_t)(p.span_hi - p.span_lo + 1) * es;
-    std::vector<char> tmp(span);
-    HIP_TRY(hipMemcpyAsync(tmp.data(), (char*)d_base + off0, span, hipMemcpyDeviceToHost, q));
-    HIP_TRY(hipStreamSynchronize(q));
     const size_t w0 = (size_t)(e[0] - g.f[0]) * es;
-    for (uint64_t w = (p.dims >= 4 ? g.f[3] : 0); w < (p.dims >= 4 ? e[3] : 1); w++)
-      for (uint64_t z = (p.dims >= 3 ? g.f[2] : 0); z < (p.dims >= 3 ? e[2] : 1); z++)
-        for (uint64_t y = (p.dims >= 2 ? g.f[1] : 0); y < (p.dims >= 2 ? e[1] : 1); y++) {
-          const int64_t o = (int64_t)g.f[0] * g.s[0] + (int64_t)y * (p.dims >= 2 ? g.s[1] : 0) +
-                            (int64_t)z * (p.dims >= 3 ? g.s[2] : 0) + (int64_t)w * (p.dims >= 4 ? g.s[3] : 0);
-          memcpy((char*)h_base + o * (int64_t)es, tmp.data() + (o * (int64_t)es - (int64_t)off0), w0);
-        }
+    const size_t nrows = p.dims >= 2 ? (size_t)(e[1] - g.f[1]) : 1;
+    const size_t pitch = nrows > 1 ? (size_t)g.s[1] * es : w0;
+    const uint64_t z0 = p.dims >= 3 ? g.f[2] : 0, z1 = p.dims >= 3 ? e[2] : 1;
+    const uint64_t v0 = p.dims >= 4 ? g.f[3] : 0, v1 = p.dims >= 4 ? e[3] : 1;
+    std::vector<char> tmp(w0 * nrows * (size_t)((z1 - z0) * (v1 - v0)));
+    auto slice_off = [&](uint64_t z, uint64_t w) {
+      return (int64_t)g.f[0] * g.s[0] + (int64_t)(p.dims >= 2 ? g.f[1] : 0) * (p.dims >= 2 ? g.s[1] : 0) +
+             (int64_t)z * (p.dims >= 3 ? g.s[2] : 0) + (int64_t)w * (p.dims >= 4 ? g.s[3] : 0);
+    };
+    size_t k = 0;
+    for (uint64_t w = v0; w < v1; w++)
+      for (uint64_t z = z0; z < z1; z++, k++)
+        HIP_TRY(hipMemcpy2DAsync(tmp.data() + k * w0 * nrows, w0, (char*)d_base + slice_off(z, w) * (int64_t)es, pitch,
+                                 w0, nrows, hipMemcpyDeviceToHost, q));
+    HIP_TRY(hipStreamSynchronize(q));
+    k = 0;
+    for (uint64_t w = v0; w < v1; w++)
+      for (uint64_t z = z0; z < z1; z++, k++)
+        for (size_t y = 0; y < nrows; y++)
+          memcpy((char*)h_base + (slice_off(z, w) + (int64_t)y * (p.dims >= 2 ? g.s[1] : 0)) * (int64_t)es,
+                 tmp.data() + (k * nrows + y) * w0, w0);
     return 1;
   }
   // row-wise 2D copies, one per (z, w) slice
@@ -1078,10 +1166,24 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
   return 1;
 }
 
-static bool index_matches(const zfp_hip_index* x, const Plan& p, uint64_t bit_offset, int device)
+// the index was made for this stream: same codec settings, layout, bit offset
+// and device, and the stream's fingerprint over the index's bit count agrees
+static bool index_matches(Ctx* c, const zfp_hip_index* x, const Plan& p, const uint64_t* words, bool dev_stream,
+                          uint64_t capacity_words, uint64_t bit_offset)
 {
-  return x && x->d_len && x->nblocks == p.g.nblocks && x->start_bit == bit_offset && x->device == device &&
-         x->per_wave == (p.dims == 4 ? kBlocks4PerWave : 64u);
+  if (!(x && x->d_len && x->nblocks == p.g.nblocks && x->start_bit == bit_offset && x->device == c->device &&
+        x->per_wave == (p.dims == 4 ? kBlocks4PerWave : 64u) && x->minbits == p.cp.minbits &&
+        x->maxbits == p.cp.maxbits && x->maxprec == p.cp.maxprec && x->minexp == p.cp.minexp && x->type == p.type &&
+        x->dims == p.dims))
+    return false;
+  if (((bit_offset + x->total_bits + 63) >> 6) > capacity_words)
+    return false;
+  uint64_t fp = 0;
+  if (!stream_fingerprint(c, words, dev_stream, bit_offset, x->total_bits, &fp)) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return fp == x->fp;
 }
 
 // ---------------------------------------------------------------------------
@@ -1224,8 +1326,13 @@ static int compress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, co
   uint64_t* d_words = (uint64_t*)c->words.p;
   const uint32_t per_wave = p.dims == 4 ? kBlocks4PerWave : 64u;
   const bool var_index = !p.fixed && index;
-  if (var_index && !index_reserve(index, p.g.nblocks, (p.g.nblocks + per_wave - 1) / per_wave))
-    return 0;
+  if (var_index) {
+    // the index describes no stream until this one is complete
+    index->start_bit = ~0ull;
+    index->nblocks = 0;
+    if (!index_reserve(index, p.g.nblocks, (p.g.nblocks + per_wave - 1) / per_wave))
+      return 0;
+  }
   EventSet ev_in(ns), ev_k(ns);
   std::vector<uint64_t> wa(ns), wb(ns);  // stream words [wa, wb) of slab s, relative to W0
   PipeSync ps;
@@ -1302,8 +1409,10 @@ static int compress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, co
     ps.fail_with(g_err.c_str());
   up.join();
   down.join();
+  // every queued copy has finished before the call returns, failed or not
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->side[0]);
+  (void)hipStreamSynchronize(c->side[1]);
   if (!ok)
     return 0;
   if (ps.failed)
@@ -1314,6 +1423,9 @@ static int compress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, co
     index->nwaves = (p.g.nblocks + per_wave - 1) / per_wave;
     index->per_wave = per_wave;
     index->total_bits = off - bit_offset;
+    index_stamp(index, p);
+    if (!stream_fingerprint(c, words, false, bit_offset, index->total_bits, &index->fp))
+      return 0;
     index->start_bit = bit_offset;
   }
   *end_bit = off;
@@ -1393,8 +1505,10 @@ static int decompress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, 
     ps.fail_with(g_err.c_str());
   up.join();
   down.join();
+  // every queued copy has finished before the call returns, failed or not
   (void)hipStreamSynchronize(c->stream);
   (void)hipStreamSynchronize(c->side[0]);
+  (void)hipStreamSynchronize(c->side[1]);
   if (!ok)
     return 0;
   if (ps.failed)
@@ -1519,8 +1633,12 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   record_timing(c);
-  if (index && !p.fixed)
+  if (index && !p.fixed) {
+    index_stamp(index, p);
+    if (!stream_fingerprint(c, words, dev_stream, bit_offset, total, &index->fp))
+      return 0;
     index->start_bit = bit_offset;
+  }
   *end_bit = end;
   return 1;
 }
@@ -1547,9 +1665,11 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
     *end_bit = bit_offset;
     return 1;
   }
+  const bool dev_field = is_device_ptr(field_base);
+  const bool dev_stream = is_device_ptr(words);
   // a variable-rate stream without a matching index (made by another
-  // process, another library, or for another position) is scanned
-  const bool have_index = !p.fixed && index_matches(index, p, bit_offset, c->device);
+  // process, another library, or for another stream or position) is scanned
+  const bool have_index = !p.fixed && index_matches(c, index, p, words, dev_stream, capacity_words, bit_offset);
   const bool scan = !p.fixed && !have_index;
   const uint64_t avail = capacity_words > W0 ? capacity_words - W0 : 0;
   uint64_t nwords;
@@ -1560,8 +1680,6 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
   else
     nwords = (g0 + p.g.nblocks * (uint64_t)p.max_len + 63) / 64 + 1;
   nwords = std::min<uint64_t>(nwords, avail);
-  const bool dev_field = is_device_ptr(field_base);
-  const bool dev_stream = is_device_ptr(words);
   if (p.fixed && !dev_field && !dev_stream && !getenv("ZFP_HIP_NO_PIPE")) {
     std::vector<Slab> sl;
     if (make_slabs(job, field_base, p, 1, sl)) {
@@ -1652,6 +1770,9 @@ int zfp_hip_index_build(const zfp_hip_job* job, const uint64_t* words, uint64_t 
   } else if (!scan_index(c, p, d_in, nwords, g0, index)) {
     return 0;
   }
+  index_stamp(index, p);
+  if (!stream_fingerprint(c, words, is_device_ptr(words), bit_offset, index->total_bits, &index->fp))
+    return 0;
   index->start_bit = bit_offset;
   return 1;
 }
@@ -1668,23 +1789,32 @@ void zfp_hip_index_free(zfp_hip_index* index)
 
 uint64_t zfp_hip_index_blocks(const zfp_hip_index* index) { return index ? index->nblocks : 0; }
 
+// exported index: a 10-word head (tag, layout, bit count, fingerprint, codec
+// settings), the per-block lengths, the per-wave bases
+constexpr size_t kIndexHead = 80;
+constexpr uint64_t kIndexTag = 0x337a6678646e69ull;  // "indxfz3"
+
 size_t zfp_hip_index_export(const zfp_hip_index* index, void* buffer, size_t capacity)
 {
   if (!index)
     return 0;
-  size_t need = 48 + index->nblocks * 2 + index->nwaves * 8;
+  size_t need = kIndexHead + index->nblocks * 2 + index->nwaves * 8;
   if (!buffer)
     return need;
   if (capacity < need)
     return 0;
   uint64_t* h = (uint64_t*)buffer;
-  h[0] = 0x327a6678646e69ull;  // tag ("indxfz2")
+  h[0] = kIndexTag;
   h[1] = index->nblocks;
   h[2] = index->nwaves;
   h[3] = index->total_bits;
   h[4] = index->per_wave;
   h[5] = index->start_bit;
-  char* q = (char*)buffer + 48;
+  h[6] = index->fp;
+  h[7] = ((uint64_t)index->maxbits << 32) | index->minbits;
+  h[8] = ((uint64_t)(uint32_t)index->minexp << 32) | index->maxprec;
+  h[9] = ((uint64_t)(uint32_t)index->dims << 32) | (uint32_t)index->type;
+  char* q = (char*)buffer + kIndexHead;
   if (index->nblocks && hipMemcpy(q, index->d_len, index->nblocks * 2, hipMemcpyDeviceToHost) != hipSuccess)
     return 0;
   q += index->nblocks * 2;
@@ -1695,10 +1825,10 @@ size_t zfp_hip_index_export(const zfp_hip_index* index, void* buffer, size_t cap
 
 zfp_hip_index* zfp_hip_index_import(const void* buffer, size_t bytes)
 {
-  if (!buffer || bytes < 48)
+  if (!buffer || bytes < kIndexHead)
     return nullptr;
   const uint64_t* h = (const uint64_t*)buffer;
-  if (h[0] != 0x327a6678646e69ull || bytes < 48 + h[1] * 2 + h[2] * 8)
+  if (h[0] != kIndexTag || h[1] > (1ull << 32) || h[2] > h[1] || bytes < kIndexHead + h[1] * 2 + h[2] * 8)
     return nullptr;
   zfp_hip_index* x = new zfp_hip_index;
   x->nblocks = h[1];
@@ -1706,8 +1836,15 @@ zfp_hip_index* zfp_hip_index_import(const void* buffer, size_t bytes)
   x->total_bits = h[3];
   x->per_wave = (uint32_t)h[4];
   x->start_bit = h[5];
+  x->fp = h[6];
+  x->minbits = (uint32_t)h[7];
+  x->maxbits = (uint32_t)(h[7] >> 32);
+  x->maxprec = (uint32_t)h[8];
+  x->minexp = (int32_t)(uint32_t)(h[8] >> 32);
+  x->type = (int32_t)(uint32_t)h[9];
+  x->dims = (int32_t)(uint32_t)(h[9] >> 32);
   (void)hipGetDevice(&x->device);
-  const char* q = (const char*)buffer + 48;
+  const char* q = (const char*)buffer + kIndexHead;
   if ((x->nblocks && hipMalloc(&x->d_len, x->nblocks * 2) != hipSuccess) ||
       (x->nwaves && hipMalloc(&x->d_base, x->nwaves * 8) != hipSuccess)) {
     zfp_hip_index_free(x);

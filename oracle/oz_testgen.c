@@ -213,3 +213,28 @@ uint32_t oz_hash_array32(const uint32_t* a, size_t n)
 
 /* hashArray64 with unit stride (same as the word hash) */
 uint64_t oz_hash_array64(const uint64_t* a, size_t n) { return oz_hash_words(a, n); }
+
+/* generateSmoothRandInts32 / Ints64 as the reference's end-to-end tests call
+ * them (tests/src/endtoend/zfpEndtoendBase.c:78-84: amplitude exponent
+ * intprec - 2; genSmoothRandNums.c:885-893 cast64ArrayTo32) */
+size_t oz_gen_smooth_int32(size_t min_total, int dims, int32_t* out, size_t cap)
+{
+  size_t side;
+  int64_t* v = oz_gen_smooth_ints(min_total, dims, 32 - 2, &side);
+  size_t tot = ipow(side, dims);
+  if (out && tot <= cap)
+    for (size_t i = 0; i < tot; i++) out[i] = (int32_t)v[i];
+  free(v);
+  return side;
+}
+
+size_t oz_gen_smooth_int64(size_t min_total, int dims, int64_t* out, size_t cap)
+{
+  size_t side;
+  int64_t* v = oz_gen_smooth_ints(min_total, dims, 64 - 2, &side);
+  size_t tot = ipow(side, dims);
+  if (out && tot <= cap)
+    for (size_t i = 0; i < tot; i++) out[i] = v[i];
+  free(v);
+  return side;
+}

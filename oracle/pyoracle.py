@@ -111,6 +111,9 @@ class Oracle:
         lib.oz_gen_smooth_floats.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
         lib.oz_gen_smooth_doubles.restype = ctypes.c_size_t
         lib.oz_gen_smooth_doubles.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
+        for fn in (lib.oz_gen_smooth_int32, lib.oz_gen_smooth_int64):
+            fn.restype = ctypes.c_size_t
+            fn.argtypes = [ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t]
         lib.oz_hash_words.restype = ctypes.c_uint64
         lib.oz_hash_words.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
         lib.oz_hash_array32.restype = ctypes.c_uint32
@@ -119,7 +122,9 @@ class Oracle:
 
     # ---- generator and hashes (reference tests/utils restated) ----
     def smooth_field(self, dims, dtype, min_total=1000000):
-        fn = self.lib.oz_gen_smooth_floats if dtype == np.float32 else self.lib.oz_gen_smooth_doubles
+        fn = {np.dtype(np.float32): self.lib.oz_gen_smooth_floats, np.dtype(np.float64): self.lib.oz_gen_smooth_doubles,
+              np.dtype(np.int32): self.lib.oz_gen_smooth_int32, np.dtype(np.int64): self.lib.oz_gen_smooth_int64}[
+            np.dtype(dtype)]
         side = fn(min_total, dims, None, 0)
         out = np.empty((side,) * dims, dtype=dtype)
         fn(min_total, dims, out.ctypes.data, out.size)

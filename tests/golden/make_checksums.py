@@ -2,7 +2,7 @@
 """Regenerate tests/golden/checksums.json from the reference's golden tables.
 
 Reads the numeric (key1, key2, checksum) tuples of
-  /root/reference/tests/constants/checksums/{1,2,3,4}d{Float,Double}.h
+  /root/reference/tests/constants/checksums/{1,2,3,4}d{Float,Double,Int32,Int64}.h
 and records them as data, decoded with the key layout of
   tests/utils/zfpChecksums.c:75-136 (computeKey):
     key1 = test_type << 9 | subject << 7 | zfp_mode << 4 | param
@@ -36,7 +36,7 @@ def dims_of(key2, dims):
 def main():
     table = []
     for dims in (1, 2, 3, 4):
-        for tname in ("Float", "Double"):
+        for tname in ("Float", "Double", "Int32", "Int64"):
             path = os.path.join(REF, "tests", "constants", "checksums", "%dd%s.h" % (dims, tname))
             text = open(path).read()
             for m in re.finditer(r"\{UINT64C\((0x[0-9a-f]+)\),\s*UINT64C\((0x[0-9a-f]+)\),\s*UINT64C\((0x[0-9a-f]+)\)\}", text):

@@ -40,7 +40,7 @@ def _worker(rank, world, port, backend, kw, q):
         zp = zfpy.zfp_parallel(SHAPE, "float32", nparts=8)
         zp.get_numpy_array()[...] = _field()
         out = zdist.compress_distributed(zp, **kw)
-        q.put([bytes(s) for s in out] if rank == 0 else None)
+        q.put([(bytes(s), s.block_index) for s in out] if rank == 0 else None)
     finally:
         dist.destroy_process_group()
 
@@ -68,9 +68,27 @@ def test_compress_distributed_matches_single_process(product, world, backend, kw
     zp = zfpy.zfp_parallel(SHAPE, "float32", nparts=8)
     zp.get_numpy_array()[...] = _field()
     want = [bytes(s) for s in zp.compress(nthreads=4, **kw)]
-    got = _run(world, backend, kw)
+    res = _run(world, backend, kw)
+    got = [g for g, _ in res]
     assert len(got) == len(want) == zp.get_chunkit().get_nchunks()
     assert got == want
+    # variable-rate chunks arrive with their block index and decode without the stream scan
+    import ctypes
+    from zfpy import zfpy_c
+    lib = zfpy_c._lib
+    lib.zfp_hip_last_scan.restype = ctypes.c_int
+    lib.zfp_hip_last_scan.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    zp3 = zfpy.zfp_parallel(SHAPE, "float32", nparts=8)
+    ck = zp3.get_chunkit()
+    for i, (g, blob) in enumerate(res):
+        assert (blob is None) == ("rate" in kw)
+        chunk = zfpy_c.ZfpBytes(g)
+        chunk.block_index = blob
+        zfpy_c.decompress_numpy_portion(chunk, zp3.get_raw_array(), ck, i, device=0)
+        assert lib.zfp_hip_last_scan(None, None) == 0, "chunk %d was scanned despite its index" % i
+        if blob is not None:  # the same bytes without the index are scanned
+            zfpy_c.decompress_numpy_portion(zfpy_c.ZfpBytes(g), zp3.get_raw_array(), ck, i, device=0)
+            assert lib.zfp_hip_last_scan(None, None) == 1
     # and the gathered plain bytes decompress to the single-process result
     zp2 = zfpy.zfp_parallel(SHAPE, "float32", nparts=8)
     zp2._compress_data = got

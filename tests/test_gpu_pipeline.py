@@ -67,6 +67,8 @@ def test_pipelined_stream_and_roundtrip_match_oracle(product, oracle, slabs, sha
             out, n = product.decompress(got, a.shape, dtype, mode, param, ztype=ztype, index=index)
             assert n == len(got)
             assert out.tobytes() == ref.tobytes()
+            # fixed rate, or variable rate with its index: slab boundaries known up front, pipelined
+            assert _pipelined(product) == (mode == "rate" or index is not None)
     finally:
         if product.last_index:
             product.lib.zfp_hip_index_free(product.last_index)

@@ -110,16 +110,19 @@ def _gather_worker(rank, world, port, nchunks, q):
         local = {}
         for i in zdist.rank_chunks(nchunks, world, rank):
             local[i] = zfpy.zfpy_c.ZfpBytes(bytes([i % 251]) * (100 + 37 * i))
+            if i % 2:  # variable-rate chunks carry their block index
+                local[i].block_index = bytes([(7 * i) % 256]) * (50 + i)
         out = zdist.gather_streams(local, nchunks, dst=0)
         if rank == 0:
-            q.put([bytes(s) for s in out])
+            q.put([(bytes(s), s.block_index) for s in out])
         else:
             q.put(out)
     finally:
         dist.destroy_process_group()
 
 
-def test_gather_streams_gloo_world2():
+@pytest.mark.parametrize("world", [2, 3])
+def test_gather_streams_gloo(world):
     import multiprocessing as mp
     import socket
     with socket.socket() as sk:
@@ -128,7 +131,7 @@ def test_gather_streams_gloo_world2():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     nchunks = 9
-    ps = [ctx.Process(target=_gather_worker, args=(r, 2, port, nchunks, q)) for r in range(2)]
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, nchunks, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=120) for _ in ps]
@@ -136,11 +139,12 @@ def test_gather_streams_gloo_world2():
         p.join(timeout=60)
         assert p.exitcode == 0
     root = [r for r in res if r is not None]
-    assert len(root) == 1 and res.count(None) == 1
+    assert len(root) == 1 and res.count(None) == world - 1
     got = root[0]
     assert len(got) == nchunks
-    for i, s in enumerate(got):
+    for i, (s, blob) in enumerate(got):
         assert s == bytes([i % 251]) * (100 + 37 * i)
+        assert blob == (bytes([(7 * i) % 256]) * (50 + i) if i % 2 else None)
 
 
 # ---------------- CPU: header() ----------------

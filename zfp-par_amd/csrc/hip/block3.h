@@ -95,7 +95,10 @@ struct alignas(16) Vec16 {
 // Streaming field reads (each byte is read once): ZFP_NT_LOAD marks them
 // non-temporal.
 #ifndef ZFP_NT_LOAD
-#define ZFP_NT_LOAD 0
+#define ZFP_NT_LOAD 1
+#endif
+#ifndef ZFP_NT_STORE
+#define ZFP_NT_STORE 1
 #endif
 template <typename S, int N>
 __device__ __forceinline__ Vec16<S, N> load16(const S* p)
@@ -108,6 +111,20 @@ __device__ __forceinline__ Vec16<S, N> load16(const S* p)
   return r;
 #else
   return *reinterpret_cast<const Vec16<S, N>*>(p);
+#endif
+}
+
+// streaming writes of decoded values / stream words (ZFP_NT_STORE: non-temporal)
+template <typename S, int N>
+__device__ __forceinline__ void store16(S* p, const Vec16<S, N>& q)
+{
+#if ZFP_NT_STORE && defined(__HIP_DEVICE_COMPILE__)
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  u4 x;
+  __builtin_memcpy(&x, &q, 16);
+  __builtin_nontemporal_store(x, reinterpret_cast<u4*>(p));
+#else
+  *reinterpret_cast<Vec16<S, N>*>(p) = q;
 #endif
 }
 
@@ -187,15 +204,15 @@ __device__ __forceinline__ void scatter3(const S (&v)[64], S* __restrict__ base,
 #pragma unroll
             for (int i = 0; i < 4; i++)
               q.v[i] = v[16 * k + 4 * j + i];
-            *reinterpret_cast<Vec16<S, 4>*>(r) = q;
+            store16<S, 4>(r, q);
           } else {
             Vec16<S, 2> q0, q1;
             q0.v[0] = v[16 * k + 4 * j + 0];
             q0.v[1] = v[16 * k + 4 * j + 1];
             q1.v[0] = v[16 * k + 4 * j + 2];
             q1.v[1] = v[16 * k + 4 * j + 3];
-            *reinterpret_cast<Vec16<S, 2>*>(r) = q0;
-            *reinterpret_cast<Vec16<S, 2>*>(r + 2) = q1;
+            store16<S, 2>(r, q0);
+            store16<S, 2>(r + 2, q1);
           }
         } else {
 #pragma unroll

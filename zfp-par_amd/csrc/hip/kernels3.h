@@ -90,10 +90,7 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m
 // d = sw / 2 (0 for d = 1).
 __host__ __device__ constexpr uint32_t slot_dwords_for(uint32_t lim) { return (lim + 95u) / 32u + 1u; }
 
-// the stream is written once and not read back by this kernel
-#ifndef ZFP_NT_STORE
-#define ZFP_NT_STORE 0
-#endif
+// (ZFP_NT_STORE, block3.h: the stream is written once and not read back)
 // wave priority while issuing the field loads / the copy-out (0: unchanged)
 #ifndef ZFP_ENC_PRIO
 #define ZFP_ENC_PRIO 0
@@ -615,6 +612,32 @@ struct DecodeArgs {
   uint32_t packw;
 };
 
+// Copy n 64-bit items to LDS, item t = lane + 64 i per lane: U loads are issued
+// before their stores, so U memory round trips overlap (a loop with a store
+// after every load waits out one full round trip per item).
+#ifndef ZFP_STAGE_BATCH
+#define ZFP_STAGE_BATCH 8
+#endif
+template <int U = ZFP_STAGE_BATCH, typename Load, typename Store>
+__device__ __forceinline__ void stage_batched(uint32_t n, Load&& load, Store&& store)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t base = 0; base < n; base += 64u * U) {
+    uint64_t v[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = base + lane + 64u * u;
+      v[u] = t < n ? load(t) : 0ull;
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const uint32_t t = base + lane + 64u * u;
+      if (t < n)
+        store(t, v[u]);
+    }
+  }
+}
+
 // Each lane's block is staged into its own LDS slot (odd stride: lanes reading
 // the same offset of their blocks hit different banks), funnel-shifted so the
 // block starts at bit 0.  Staging is cooperative: thread t copies word j of
@@ -661,25 +684,34 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
   __builtin_amdgcn_wave_barrier();
   const uint64_t nb = live ? ((g.nblocks - first) < 64 ? (g.nblocks - first) : 64) : 0;
   const uint32_t pairs = (uint32_t)nb * a.W;
+  auto slot_of = [&](uint32_t t) -> uint64_t* {
+    const uint32_t l = __umulhi(t, a.wmagic);
+    return wslot + (size_t)l * a.swp + (t - l * a.W);
+  };
   if (!a.var && (G & 63) == 0 && (a.maxbits & 63) == 0) {
     // word-aligned fixed rate (wave-uniform): block l starts at word l * bw
     const uint32_t bw = a.maxbits >> 6;
-    for (uint32_t t = lane; t < pairs; t += 64) {
-      const uint32_t l = __umulhi(t, a.wmagic);
-      const uint32_t j = t - l * a.W;
-      const uint64_t gw = W0 + l * bw + j;
-      wslot[l * a.swp + j] = gw < a.in_words ? a.in[gw] : 0ull;
-    }
-  } else
-  for (uint32_t t = lane; t < pairs; t += 64) {
-    const uint32_t l = __umulhi(t, a.wmagic);
-    const uint32_t j = t - l * a.W;
-    const uint32_t sb = sbit[wv * 64 + l];
-    const uint64_t gw = W0 + (sb >> 6) + j;
-    const uint32_t sh = sb & 63;
-    const uint64_t lo = gw < a.in_words ? a.in[gw] : 0ull;
-    const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
-    wslot[(size_t)l * a.swp + j] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    stage_batched(
+        pairs,
+        [&](uint32_t t) {
+          const uint32_t l = __umulhi(t, a.wmagic);
+          const uint64_t gw = W0 + l * bw + (t - l * a.W);
+          return gw < a.in_words ? a.in[gw] : 0ull;
+        },
+        [&](uint32_t t, uint64_t v) { *slot_of(t) = v; });
+  } else {
+    stage_batched(
+        pairs,
+        [&](uint32_t t) {
+          const uint32_t l = __umulhi(t, a.wmagic);
+          const uint32_t sb = sbit[wv * 64 + l];
+          const uint64_t gw = W0 + (sb >> 6) + (t - l * a.W);
+          const uint32_t sh = sb & 63;
+          const uint64_t lo = gw < a.in_words ? a.in[gw] : 0ull;
+          const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
+          return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+        },
+        [&](uint32_t t, uint64_t v) { *slot_of(t) = v; });
   }
   // Blocks longer than a short slot (wave-uniform, rare on smooth data): the
   // lane stages its whole block into an overflow slot in global memory.

@@ -244,31 +244,45 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
         atomicOr(a.error, 2u);
       return;  // wave-uniform: a one-wave workgroup
     }
-    for (uint32_t t = lane; t < nwords; t += 64) {
-      const uint64_t gw = W0 + t;
-      region[t] = gw < a.in_words ? a.in[gw] : 0ull;
-    }
+    stage_batched(
+        nwords,
+        [&](uint32_t t) {
+          const uint64_t gw = W0 + t;
+          return gw < a.in_words ? a.in[gw] : 0ull;
+        },
+        [&](uint32_t t, uint64_t v) { region[t] = v; });
     rpos = sbit[qd];
     rbase = region;
   } else if (!a.var && (G & 63) == 0 && (a.maxbits & 63) == 0) {
     // word-aligned fixed rate (wave-uniform): block l starts at word l * bw
     const uint32_t bw = a.maxbits >> 6;
-    for (uint32_t t = lane; t < pairs; t += 64) {
-      const uint32_t l = __umulhi(t, a.wmagic);
-      const uint32_t j = t - l * a.W;
-      const uint64_t gw = W0 + l * bw + j;
-      region[l * a.swp + j] = gw < a.in_words ? a.in[gw] : 0ull;
-    }
-  } else
-  for (uint32_t t = lane; t < pairs; t += 64) {
-    const uint32_t l = __umulhi(t, a.wmagic);
-    const uint32_t j = t - l * a.W;
-    const uint32_t sb = sbit[l];
-    const uint64_t gw = W0 + (sb >> 6) + j;
-    const uint32_t sh = sb & 63;
-    const uint64_t lo = gw < a.in_words ? a.in[gw] : 0ull;
-    const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
-    region[(size_t)l * a.swp + j] = sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+    stage_batched(
+        pairs,
+        [&](uint32_t t) {
+          const uint32_t l = __umulhi(t, a.wmagic);
+          const uint64_t gw = W0 + l * bw + (t - l * a.W);
+          return gw < a.in_words ? a.in[gw] : 0ull;
+        },
+        [&](uint32_t t, uint64_t v) {
+          const uint32_t l = __umulhi(t, a.wmagic);
+          region[l * a.swp + (t - l * a.W)] = v;
+        });
+  } else {
+    stage_batched(
+        pairs,
+        [&](uint32_t t) {
+          const uint32_t l = __umulhi(t, a.wmagic);
+          const uint32_t sb = sbit[l];
+          const uint64_t gw = W0 + (sb >> 6) + (t - l * a.W);
+          const uint32_t sh = sb & 63;
+          const uint64_t lo = gw < a.in_words ? a.in[gw] : 0ull;
+          const uint64_t hi = gw + 1 < a.in_words ? a.in[gw + 1] : 0ull;
+          return sh ? (lo >> sh) | (hi << (64 - sh)) : lo;
+        },
+        [&](uint32_t t, uint64_t v) {
+          const uint32_t l = __umulhi(t, a.wmagic);
+          region[(size_t)l * a.swp + (t - l * a.W)] = v;
+        });
   }
   __syncthreads();
   WordReader rd;

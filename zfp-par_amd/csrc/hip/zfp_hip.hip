@@ -1432,29 +1432,47 @@ static int compress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, co
   return 1;
 }
 
-// fixed rate: slab s's words are known before any kernel runs
+// Slab s's stream words are known before any kernel runs: fixed rate
+// analytically, variable rate from the block index (the start of the slab's
+// first wave; slabs hold whole waves), whose per-slab bases are read back
+// first.  Every slab decodes against the chunk's whole stream image, with its
+// view of the index, once its own words have arrived.
 template <typename S>
 static int decompress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, void* field_base,
-                            const uint64_t* words, uint64_t capacity_words, uint64_t bit_offset, uint64_t* end_bit)
+                            const uint64_t* words, uint64_t capacity_words, uint64_t bit_offset,
+                            const zfp_hip_index* index, uint64_t* end_bit)
 {
   const size_t es = sizeof(S);
   const size_t ns = sl.size();
   const uint64_t W0 = bit_offset >> 6;
+  const uint32_t g0 = (uint32_t)(bit_offset & 63);
   const uint64_t avail = capacity_words > W0 ? capacity_words - W0 : 0;
   const uint64_t mb = p.cp.maxbits;
-  const uint64_t nwords = std::min<uint64_t>(((bit_offset & 63) + p.g.nblocks * mb + 63) / 64 + 1, avail);
+  const uint32_t per_wave = p.dims == 4 ? kBlocks4PerWave : 64u;
+  const uint64_t total = p.fixed ? p.g.nblocks * mb : index->total_bits;
+  const uint64_t nwords = std::min<uint64_t>((g0 + total + 63) / 64 + 1, avail);
   if (!ensure(c->field, (size_t)(p.span_hi - p.span_lo + 1) * es) || !ensure(c->words, nwords * 8 + 8) ||
       !ensure_side_streams(c))
     return 0;
   char* d_img = (char*)c->field.p - p.span_lo * (int64_t)es;
   uint64_t* d_words = (uint64_t*)c->words.p;
   EventSet ev_in(ns), ev_k(ns);
+  // bit offset of slab s's first block relative to the chunk's first block
+  std::vector<uint64_t> base(ns + 1, total);
+  for (size_t s = 0; s < ns; s++) {
+    if (p.fixed)
+      base[s] = sl[s].b0 * mb;
+    else
+      HIP_TRY(hipMemcpyAsync(&base[s], index->d_base + sl[s].b0 / per_wave, 8, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_TRY(hipStreamSynchronize(c->stream));
   // stream words [wa, wb) relative to W0 read by slab s (one word of lookahead)
   std::vector<uint64_t> wa(ns), wb(ns);
   for (size_t s = 0; s < ns; s++) {
-    const uint64_t o = bit_offset + sl[s].b0 * mb;
-    wa[s] = (o >> 6) - W0;
-    wb[s] = std::min<uint64_t>(((o + sl[s].p.g.nblocks * mb + 63) >> 6) + 1 - W0, nwords);
+    if (base[s] > base[s + 1] || base[s + 1] > total)
+      return fail("zfp_hip_decompress: block index inconsistent with the slab layout");
+    wa[s] = (g0 + base[s]) >> 6;
+    wb[s] = std::min<uint64_t>(((g0 + base[s + 1] + 63) >> 6) + 1, nwords);
   }
   PipeSync ps;
   std::thread up([&] {
@@ -1491,8 +1509,23 @@ static int decompress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, 
       ok = fail("hipStreamWaitEvent failed");
       break;
     }
-    const uint64_t o = bit_offset + sl[s].b0 * mb;
-    ok = launch_decode<S>(c, sl[s].p, (S*)d_img, d_words + wa[s], wb[s] - wa[s], (uint32_t)(o & 63), nullptr);
+    if (p.fixed) {
+      const uint64_t o = bit_offset + sl[s].b0 * mb;
+      ok = launch_decode<S>(c, sl[s].p, (S*)d_img, d_words + wa[s], wb[s] - wa[s], (uint32_t)(o & 63), nullptr);
+    } else {
+      // the slab's part of the chunk's index (bases stay relative to the chunk)
+      zfp_hip_index view;
+      view.device = c->device;
+      view.nblocks = sl[s].p.g.nblocks;
+      view.nwaves = (sl[s].p.g.nblocks + per_wave - 1) / per_wave;
+      view.per_wave = per_wave;
+      view.total_bits = base[s + 1] - base[s];
+      view.d_len = index->d_len + sl[s].b0;
+      view.d_base = index->d_base + sl[s].b0 / per_wave;
+      ok = launch_decode<S>(c, sl[s].p, (S*)d_img, d_words, nwords, g0, &view);
+      view.d_len = nullptr;  // a view: nothing to free
+      view.d_base = nullptr;
+    }
     if (!ok)
       break;
     if (hipEventRecord(ev_k.ev[s], c->stream) != hipSuccess) {
@@ -1513,7 +1546,7 @@ static int decompress_slabs(Ctx* c, const Plan& p, const std::vector<Slab>& sl, 
     return 0;
   if (ps.failed)
     return fail("zfp_hip_decompress: %s", ps.err.c_str());
-  *end_bit = bit_offset + p.g.nblocks * mb;
+  *end_bit = bit_offset + total;
   return 1;
 }
 
@@ -1680,13 +1713,13 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
   else
     nwords = (g0 + p.g.nblocks * (uint64_t)p.max_len + 63) / 64 + 1;
   nwords = std::min<uint64_t>(nwords, avail);
-  if (p.fixed && !dev_field && !dev_stream && !getenv("ZFP_HIP_NO_PIPE")) {
+  if ((p.fixed || have_index) && !dev_field && !dev_stream && !getenv("ZFP_HIP_NO_PIPE")) {
     std::vector<Slab> sl;
-    if (make_slabs(job, field_base, p, 1, sl)) {
+    if (make_slabs(job, field_base, p, p.fixed ? 1 : (p.dims == 4 ? kBlocks4PerWave : 64u), sl)) {
       const auto t0 = std::chrono::steady_clock::now();
       const int ok = by_type(p, [&](auto tag) {
         using S = std::remove_pointer_t<decltype(tag)>;
-        return decompress_slabs<S>(c, p, sl, field_base, words, capacity_words, bit_offset, end_bit);
+        return decompress_slabs<S>(c, p, sl, field_base, words, capacity_words, bit_offset, index, end_bit);
       });
       t_timing.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       t_timing.kernel_ms = 0;

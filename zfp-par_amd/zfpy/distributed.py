@@ -14,8 +14,10 @@ concatenated payload.
         PCIe on the compressing rank.
   gloo (CPU tests): host bytes, as the single-process zfp_parallel returns.
 
-Variable-rate streams need no side-band data: the decoder finds the block
-starts itself (zfp_hip_index_build).
+Variable-rate chunks carry their GPU block index (ZfpBytes.block_index)
+through the gather, so the root decodes them without the stream scan; a stream
+that arrives without one (or with one for another stream) is still decoded,
+after the scan finds its block starts (zfp_hip_index_build).
 """
 import ctypes
 
@@ -37,46 +39,78 @@ def _device_for(dist, group):
     return torch.device("cpu")
 
 
-def _sizes(local, nchunks, dev, dist, group):
-    import torch
-    sizes = torch.zeros(nchunks, dtype=torch.int64, device=dev)
-    for i, s in local.items():
-        sizes[i] = s.numel() if hasattr(s, "numel") else len(s)
-    dist.all_reduce(sizes, op=dist.ReduceOp.SUM, group=group)
-    return sizes.cpu().numpy()
+def _blob(s):
+    """The block-index blob a chunk stream carries (ZfpBytes.block_index / tensor attribute), or b''."""
+    b = getattr(s, "block_index", None)
+    return bytes(b) if b else b""
 
 
 def gather_streams(local, nchunks, dst=0, group=None):
     """Gather {chunk id: stream} from every rank to `dst`; returns the list of all
-    chunk streams (bytes) in chunk order on `dst`, None elsewhere.  A stream is
-    host bytes, or a uint8 device tensor on the nccl path (gathered in HBM)."""
+    chunk streams (ZfpBytes) in chunk order on `dst`, None elsewhere.  A stream is
+    host bytes, or a uint8 device tensor on the nccl path (gathered in HBM).
+
+    Each chunk's GPU block index (variable-rate streams) travels with it, so the
+    root decodes gathered chunks without scanning them.  One all-reduce carries
+    the stream and index sizes of every chunk; then every rank sends its exact
+    payload (its streams, then its index blobs) to `dst` point to point, no
+    padding; on the root each payload is copied to the host once and every
+    chunk's bytes object is cut from that copy."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     dev = _device_for(dist, group)
-    sz = _sizes(local, nchunks, dev, dist, group)
-    per_rank = [int(sz[rank_chunks(nchunks, world, r)].sum()) for r in range(world)]
-    mx = max(per_rank) if per_rank else 0
+    mine = rank_chunks(nchunks, world, rank)
+    sizes = torch.zeros(2 * nchunks, dtype=torch.int64, device=dev)
+    blobs = {i: _blob(local[i]) for i in mine}
+    for i in mine:
+        s = local[i]
+        sizes[i] = s.numel() if hasattr(s, "numel") else len(s)
+        sizes[nchunks + i] = len(blobs[i])
+    dist.all_reduce(sizes, op=dist.ReduceOp.SUM, group=group)
+    sz = sizes.cpu().numpy()
+    per_rank = [int(sz[rank_chunks(nchunks, world, r)].sum() + sz[[nchunks + i for i in rank_chunks(nchunks, world, r)]].sum())
+                for r in range(world)]
     pieces = []
-    for i in rank_chunks(nchunks, world, rank):
+    for i in mine:
         s = local[i]
         pieces.append(s.to(dev) if isinstance(s, torch.Tensor) else
-                      torch.from_numpy(np.frombuffer(bytes(s), dtype=np.uint8).copy()).to(dev))
-    if per_rank[rank] < mx:
-        pieces.append(torch.zeros(mx - per_rank[rank], dtype=torch.uint8, device=dev))
-    send = torch.cat(pieces) if pieces else torch.zeros(mx, dtype=torch.uint8, device=dev)
-    recv = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == dst else None
-    dist.gather(send, gather_list=recv, dst=dst, group=group)
+                      torch.frombuffer(bytearray(s), dtype=torch.uint8).to(dev))
+    for i in mine:
+        if blobs[i]:
+            pieces.append(torch.frombuffer(bytearray(blobs[i]), dtype=torch.uint8).to(dev))
+    send = torch.cat(pieces) if pieces else torch.zeros(0, dtype=torch.uint8, device=dev)
+    recv = None
+    ops = []
+    if rank == dst:
+        recv = [send if r == rank else torch.empty(per_rank[r], dtype=torch.uint8, device=dev) for r in range(world)]
+        ops = [dist.P2POp(dist.irecv, recv[r], r, group) for r in range(world) if r != rank and per_rank[r]]
+    elif per_rank[rank]:
+        ops = [dist.P2POp(dist.isend, send, dst, group)]
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
     if rank != dst:
         return None
     out = [None] * nchunks
     for r in range(world):
-        buf = recv[r].cpu().numpy().tobytes()  # one device-to-host copy per rank payload, on the root
+        if recv[r].device.type == "cpu":
+            host = recv[r].numpy()
+        else:  # one device-to-host copy per rank payload
+            host = np.empty(per_rank[r], dtype=np.uint8)
+            torch.from_numpy(host).copy_(recv[r])
+        view = memoryview(host)
+        ids = rank_chunks(nchunks, world, r)
         off = 0
-        for i in rank_chunks(nchunks, world, r):
+        for i in ids:
             n = int(sz[i])
-            out[i] = ZfpBytes(buf[off:off + n])
+            out[i] = ZfpBytes(view[off:off + n])
+            off += n
+        for i in ids:
+            n = int(sz[nchunks + i])
+            if n:
+                out[i].block_index = bytes(view[off:off + n])
             off += n
     return out
 
@@ -106,7 +140,9 @@ def compress_chunk_to_device(zp, ichunk, tolerance=-1, rate=-1, precision=-1, de
         n = lib.zfp_compress_chunk(stream, cp, field)
         if n == 0:
             raise RuntimeError("Failed to write to stream")
-        return buf[:n]
+        out = buf[:n]
+        out.block_index = zfpy_c._export_index(stream)  # variable rate: travels with the chunk
+        return out
     finally:
         lib.zfp_field_free(field)
         lib.zfp_stream_close(stream)

@@ -48,6 +48,16 @@ def test_block_codec_matches_oracle_all_modes(oracle_obj):
     assert r.stdout.count(" 0/3000 bad") == 32, r.stdout
 
 
+def test_plane_decoder_dense_switch_matches_reference_loop(tmp_path):
+    """decode_planes32 leaving its 32-bit body after any slow plane (the switch a wave
+    takes after a dense plane), against the same reference streams."""
+    exe = os.path.join(str(tmp_path), "plane_emu_dense")
+    subprocess.check_call(["g++", "-O2", "-std=c++17", "-DZFP_DEC32_DENSE=0", "-I" + os.path.join(EMU, "stub"),
+                           "-I" + HIP, "-o", exe, os.path.join(EMU, "plane_emu.cpp"), "-lm"])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_plane_coder_matches_reference_loop(tmp_path):
     """code_planes vs a literal restatement of encode.c:92-132 on adversarial planes."""
     r = subprocess.run([_build(str(tmp_path), "plane_emu.cpp")], capture_output=True, text=True, timeout=600)

@@ -1081,6 +1081,10 @@ __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_
 #ifndef ZFP_DEC32
 #define ZFP_DEC32 1
 #endif
+// more lanes than this in a plane's slow path: the rest of the block without the 32-bit body
+#ifndef ZFP_DEC32_DENSE
+#define ZFP_DEC32_DENSE 16
+#endif
 template <bool IMP = true>
 __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_t* sq, uint32_t budget,
                                                     uint32_t maxprec, uint64_t (&P)[32])
@@ -1134,11 +1138,18 @@ __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_
       n += one ? np : 0u;
     }
     const bool slow = act && !fast;
-    if (__builtin_amdgcn_ballot_w64(slow) != 0) {
+    const uint64_t sm = __builtin_amdgcn_ballot_w64(slow);
+    if (sm != 0) {
       if (slow) {
         uint32_t b = bits;
         P[k] = decode_plane64<IMP>(r, sq, b, n);
         bits = b;
+      }
+      // dense planes (long sections: reversible, high precision): from here on
+      // decode_plane64 alone, without the 32-bit attempt first
+      if (__popcll(sm) > ZFP_DEC32_DENSE) {
+        m32 = false;
+        ksw = k - 1;
       }
     }
   }

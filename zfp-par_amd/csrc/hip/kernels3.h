@@ -44,7 +44,7 @@ __device__ __forceinline__ uint32_t wave_incl_scan(uint32_t x)
 // per thread of the 256-thread group) and the wave's zeroed slot region.
 __device__ __forceinline__ void encode_prologue(uint32_t* lut, uint64_t* wslot, uint32_t words)
 {
-  lut[threadIdx.x] = dbl_entry(threadIdx.x);
+  lut[threadIdx.x] = kCoderTables.dbl[threadIdx.x];
   const int lane = threadIdx.x & 63;
   uint4* z = reinterpret_cast<uint4*>(wslot);
   for (uint32_t i = lane; i < words / 2; i += 64)
@@ -52,27 +52,6 @@ __device__ __forceinline__ void encode_prologue(uint32_t* lut, uint64_t* wslot, 
   if ((words & 1) && lane == 0)
     wslot[words - 1] = 0;
   __syncthreads();
-}
-
-#ifndef ZFP_EARLY_GATHER
-#define ZFP_EARLY_GATHER 1
-#endif
-// Wave-local prologue: the wave writes all 256 table entries itself (the other
-// waves of the group write the same values), so only its own LDS writes must
-// have landed -- no workgroup barrier, and loads issued before it stay in flight.
-__device__ __forceinline__ void encode_prologue_wave(uint32_t* lut, uint64_t* wslot, uint32_t words)
-{
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int i = 0; i < 4; i++)
-    lut[lane + 64 * i] = dbl_entry(lane + 64 * i);
-  uint4* z = reinterpret_cast<uint4*>(wslot);
-  for (uint32_t i = lane; i < words / 2; i += 64)
-    z[i] = make_uint4(0, 0, 0, 0);
-  if ((words & 1) && lane == 0)
-    wslot[words - 1] = 0;
-  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only (vmcnt/expcnt at max)
-  __builtin_amdgcn_wave_barrier();
 }
 
 // floor(i / d) for i < 2^20, d < 2^12 with m = ceil(2^32 / d) (m = 0 for d = 1)
@@ -325,6 +304,10 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t x)
 // lane of the wave with the same arguments.
 __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
 {
+#ifdef ZFP_LB_FAKE
+  // experiment builds only: no waiting (wrong stream, inside the buffer) -- the look-back's cost
+  return w * (uint64_t)agg;
+#endif
   const uint32_t lane = threadIdx.x & 63u;
   if (w == 0) {
     if (lane == 0)

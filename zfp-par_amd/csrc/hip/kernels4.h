@@ -51,9 +51,8 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   uint32_t* wrt = off + kBlocks4PerWave;
   uint64_t* region = lds + kEnc4HeadWords;
   const uint32_t lane = threadIdx.x;
-#pragma unroll
-  for (uint32_t i = 0; i < 4; i++)
-    lut[lane + 64 * i] = dbl_entry(lane + 64 * i);
+  // the doubled-ones table from device memory (CoderTables.dbl), one 16-byte load per lane
+  reinterpret_cast<uint4*>(lut)[lane] = reinterpret_cast<const uint4*>(kCoderTables.dbl)[lane];
   tab[lane] = kOrderTab4.t[lane];
 
   const uint64_t nwaves = (g.nblocks + kBlocks4PerWave - 1) / kBlocks4PerWave;
@@ -147,7 +146,7 @@ __global__ __launch_bounds__(64) void encode4_patch(const S* __restrict__ data, 
   const uint32_t lane = threadIdx.x;
 #pragma unroll
   for (uint32_t i = 0; i < 4; i++)
-    lut[lane + 64 * i] = dbl_entry(lane + 64 * i);
+    lut[lane + 64 * i] = kCoderTables.dbl[lane + 64 * i];
   tab[lane] = kOrderTab4.t[lane];
   const uint32_t qd = lane >> 2, r = lane & 3u;
   const uint64_t e = (uint64_t)blockIdx.x * kBlocks4PerWave + qd;

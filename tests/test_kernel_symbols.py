@@ -96,3 +96,59 @@ def test_every_host_kernel_stub_has_gfx950_code():
     assert len(host) > 20, "host kernel stubs not found (%d)" % len(host)
     missing = sorted(host - device)
     assert not missing, "kernels launched by the host without device code:\n  " + "\n  ".join(missing[:20])
+
+
+def _kernel_scratch(lib_bytes):
+    """{kernel: private_segment_fixed_size} from the gfx950 kernel descriptors (.kd)."""
+    secs = {nm: (off, size) for nm, _, off, size, _ in _sections(lib_bytes)}
+    off, size = secs[".hip_fatbin"]
+    fb = lib_bytes[off: off + size]
+    out, i = {}, 0
+    while True:
+        j = fb.find(MAGIC, i)
+        if j < 0:
+            break
+        n, = struct.unpack_from("<Q", fb, j + 24)
+        p = j + 32
+        for _ in range(n):
+            o, sz, tl = struct.unpack_from("<QQQ", fb, p)
+            p += 24
+            triple = fb[p: p + tl].decode()
+            p += tl
+            if "gfx950" not in triple or not sz:
+                continue
+            elf = fb[j + o: j + o + sz]
+            shoff, = struct.unpack_from("<Q", elf, 0x28)
+            shentsize, shnum, shstrndx = struct.unpack_from("<HHH", elf, 0x3A)
+            hdrs = [struct.unpack_from("<IIQQQQIIQQ", elf, shoff + k * shentsize) for k in range(shnum)]
+            for h in hdrs:
+                if h[1] not in (2, 11):
+                    continue
+                stro = hdrs[h[6]][4]
+                for k in range(h[5] // 24):
+                    st_name, _, _, shndx, value, _ = struct.unpack_from("<IBBHQQ", elf, h[4] + k * 24)
+                    nm = elf[stro + st_name: elf.index(b"\0", stro + st_name)].decode() if st_name else ""
+                    if not nm.endswith(".kd") or shndx == 0 or shndx >= len(hdrs):
+                        continue
+                    sec = hdrs[shndx]
+                    kd = sec[4] + (value - sec[3])  # file offset of the descriptor
+                    out[nm[:-3]] = struct.unpack_from("<I", elf, kd + 4)[0]
+        i = j + len(MAGIC)
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libzfp_hip.so not built")
+def test_hot_kernels_use_no_scratch():
+    """The float kernels (C2/C4/C5 paths) and the f64 decoders without short
+    slots keep their plane registers in VGPRs: no private (scratch) segment.
+    Scratch here means an unrolled plane loop fell back to memory (it did once:
+    LLVM's pragma-unroll threshold), which costs HBM traffic on every launch."""
+    sc = _kernel_scratch(open(LIB, "rb").read())
+    assert len(sc) > 20
+    hot = {k: v for k, v in sc.items()
+           if re.match(r"_ZN7zfp_amd(15encode3_(aligned|general)|7decode3|7encode4|7decode4)If", k)}
+    assert len(hot) >= 8, sorted(sc)[:10]
+    assert all(v == 0 for v in hot.values()), {k: v for k, v in hot.items() if v}
+    # f64 decoders without short slots: P[32] must stay in registers
+    dnon = {k: v for k, v in sc.items() if k.startswith("_ZN7zfp_amd7decode3Id") and k.endswith("Lb0EEEvPT_NS_8GeometryENS_11CodecParamsENS_10DecodeArgsE")}
+    assert dnon and all(v == 0 for v in dnon.values()), dnon

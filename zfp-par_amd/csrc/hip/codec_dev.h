@@ -835,9 +835,95 @@ __device__ __forceinline__ void fr_write32(int32_t Q, uint32_t v)
                         __HIP_MEMORY_SCOPE_WAVEFRONT);
 }
 
+// v1:v0 at bit address -Q: three dwords
+__device__ __forceinline__ void fr_write64(int32_t Q, uint32_t v0, uint32_t v1)
+{
+  const uint32_t a = ~(((uint32_t)(Q >> 3)) | 3u);
+  __hip_atomic_fetch_or(lds_at(a), __builtin_amdgcn_alignbit(v0, 0u, (uint32_t)Q), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+  __hip_atomic_fetch_or(lds_at(a + 4u), __builtin_amdgcn_alignbit(v1, v0, (uint32_t)Q), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+  __hip_atomic_fetch_or(lds_at(a + 8u), __builtin_amdgcn_alignbit(0u, v1, (uint32_t)Q), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+}
+
 #ifndef ZFP_FR32
 #define ZFP_FR32 1
 #endif
+#ifndef ZFP_FRU
+#define ZFP_FRU 1
+#endif
+
+// Fixed-rate plane body for the planes after the 32-bit lo form (any lane
+// with coefficients 32..63 in play): every lane codes from a 32-bit window
+// x0 = bits 0..31 of xs = N >> n,
+//   n < 32:  alignbit(Nh, pl, n)   (the plane's bits n..n+31)
+//   n >= 32: Nh >> (n - 32)        (Nh = ph & ~Sh; n == 64 gives 0)
+// and, while xs has its top one inside unit 0 (x0 < 0xffff, bits 32.. of xs
+// zero), the group bits are the lead-table expansion cut to e1 - impl bits
+// (e1 = bitlen(x0) + popcount(x0); impl: the top one is coefficient 63, whose
+// test and value are implicit), the plane's length n + e1 - impl + [n' < 64].
+// Lanes whose xs reaches past unit 0 (or is 0xffff: 33 group bits) are
+// recomputed in a wave-uniform branch from the 64-bit xs, as code_planes does.
+// No 64-bit arithmetic on the common path; the verbatim bits are pl cut to n
+// bits (n < 32) or pl and ph & Sh (Sh: the significant high coefficients).
+// Positions as in code_planes_fr32 (Q = -bit address).
+__device__ __forceinline__ void code_planes_fru(OrSlot& os, const uint32_t* lut, uint32_t sb, int32_t Q,
+                                                int32_t Qlim, uint32_t n, int kstart, const uint32_t (&Pl)[32],
+                                                const uint32_t (&Ph)[32])
+{
+  const uint32_t tdbl = lds_off(lut), tlead = tdbl + 1024u;
+  uint32_t Sh = n > 32u ? ~0u >> ((0u - n) & 31u) : 0u;
+#pragma unroll
+  for (int k = 31; k >= 0; k--) {
+    if (k > kstart)
+      continue;
+    if (k < ZFP_FR_EXIT_PLANES && __builtin_amdgcn_ballot_w64(Q > Qlim) == 0)
+      break;
+    const uint32_t pl = Pl[k], ph = Ph[k];
+    const bool hi = n >= 32u;
+    const uint32_t Nh = ph & ~Sh;
+    const uint32_t t = Nh >> (n & 31u);
+    const uint32_t x0 = hi ? t : __builtin_amdgcn_alignbit(Nh, pl, n);
+    const uint32_t x1 = hi ? 0u : t;  // bits 32..63 of xs
+    const uint32_t l0 = *lds_at(tlead + byte0_x4(x0));
+    const uint32_t l1 = *lds_at(tdbl + byte1_x4(x0));
+    const uint32_t bl = 31u - (uint32_t)__clz((int)((x0 << 1) | 1u));  // bitlen(x0) for x0 < 2^31
+    const uint32_t e1 = (uint32_t)__popc(x0) + bl;
+    const uint32_t impl = Nh >> 31;  // top one at coefficient 63 (lanes without ext)
+    uint32_t n1 = n + bl;
+    const uint32_t d = (l1 << (l0 & 31u)) | (l0 >> 5);  // (dbl(x0 & 0xffff) << 1 | 1) mod 2^32
+    uint32_t g = ubfe(d, 0u, e1 - impl);
+    uint32_t L = e1 - impl + 1u - (n1 >> 6);  // group bits: none once all 64 are significant
+    const bool ext = x0 > 0xfffeu || x1 != 0u;
+    const int32_t Qg = Q - (int32_t)n;
+    if (__builtin_amdgcn_ballot_w64(ext) != 0) {
+      // rare: xs reaches past unit 0 (or x0 == 0xffff); the other lanes take no part
+      uint32_t hb = 0;
+      if (ext) {
+        const uint32_t hx = x1 ? 63u - (uint32_t)__clz((int)x1) : 31u - (uint32_t)__clz((int)x0);  // top of xs
+        const uint32_t c = (uint32_t)__popc(x0) + (uint32_t)__popc(x1);
+        n1 = n + hx + 1u;
+        const uint32_t im = n1 >> 6;
+        L = hx + c + 2u - 2u * im;
+        // top one in unit 0 (x0 == 0xffff): the 33-bit expansion less the
+        // top pair's surplus (bit 32, and bit 31 when implicit); else unit 0
+        // whole, the surplus in a later unit, and bit 32 of the group bits
+        // the last of an all-ones unit 0's expansion
+        g = hx < 16u ? d & ~(im << 31) : d;
+        hb = hx | (im << 6) | ((x0 & 0xffffu) == 0xffffu ? 0x80u : 0u);
+      }
+      expand_event(os, lut, ExtEvent{(uint32_t)(-Qg) - sb, x0, x1, hb});
+    }
+    fr_write64(Q, hi ? pl : ubfe(pl, 0u, n), ph & Sh);  // the n verbatim bits
+    fr_write32(Qg, g);
+    const int32_t Qn = Qg - (int32_t)L;
+    Q = Qn > Qlim ? Qn : Qlim;
+    n = n1;
+    Sh = n > 32u ? ~0u >> ((0u - n) & 31u) : 0u;
+  }
+}
+
 __device__ __forceinline__ void code_planes_fr32(uint32_t* slot, uint32_t jmax, const uint32_t* lut, uint32_t pos,
                                                  uint32_t lim, const uint32_t (&Pl)[32], const uint32_t (&Ph)[32])
 {
@@ -886,8 +972,13 @@ __device__ __forceinline__ void code_planes_fr32(uint32_t* slot, uint32_t jmax, 
       }
     }
   }
-  if (!m32)
+  if (!m32) {
+#if ZFP_FRU
+    code_planes_fru(os, lut, sb, Q, Qlim, n, ksw, Pl, Ph);
+#else
     code_planes<32, false>(os, lut, (uint32_t)(-Q) - sb, lim, 32u, Pl, Ph, ksw, n);
+#endif
+  }
 #else
   code_planes<32, false>(os, lut, pos, lim, 32u, Pl, Ph);
 #endif

@@ -145,14 +145,18 @@ def test_short_slots_and_patch_pass_match_oracle_4d(product, oracle, monkeypatch
     _free_index(product)
 
 
-@pytest.mark.parametrize("pack_words", ["1666", "1100"])
+@pytest.mark.parametrize("pack_words", ["1666", "1100", "full"])
 @pytest.mark.parametrize("mode,param", [("precision", 20), ("accuracy", 1e-3), ("reversible", None)])
 def test_packed_staging_decode_matches_oracle_4d(product, oracle, monkeypatch, pack_words, mode, param):
-    """Variable-rate decode4 with each wave's blocks staged back to back
-    (opt-in, ZFP_HIP_PACK_WORDS); waves whose segment exceeds the staged words
-    (the rough half of the field) make the library repeat the launch with
-    padded slots."""
-    monkeypatch.setenv("ZFP_HIP_PACK_WORDS", pack_words)
+    """Variable-rate decode4 stages each wave's blocks back to back (the
+    default, sized for 16 worst-case blocks).  With fewer staged words forced
+    (ZFP_HIP_PACK_WORDS), waves whose segment exceeds them (the rough half of
+    the field) make the library repeat the launch with padded slots; "full":
+    padded slots only (ZFP_HIP_FULL_SLOTS)."""
+    if pack_words == "full":
+        monkeypatch.setenv("ZFP_HIP_FULL_SLOTS", "1")
+    else:
+        monkeypatch.setenv("ZFP_HIP_PACK_WORDS", pack_words)
     rng = np.random.default_rng(zlib.crc32(repr((pack_words, mode, param, 44)).encode()))
     a = _field4((12, 9, 16, 20), np.float32, rng)
     a[6:] = np.cos(np.arange(6 * 9 * 16 * 20, dtype=np.float32) * 1e-3).reshape(6, 9, 16, 20)

@@ -792,19 +792,20 @@ static int run_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, 
   // f32/f64: exchange areas shared by quad pairs (HALF), as in the encoder
   const bool half = !kIntField<S>;
   const size_t xfull = (size_t)kBlocks4PerWave * kXStride * sizeof(Int);
-  // variable rate, f32/f64: the wave's segment staged back to back in what
-  // three one-wave workgroups per SIMD leave (the decoders' VGPRs allow
-  // three); a wave whose segment does not fit makes the host repeat the
-  // launch with padded slots
-  // Off by default: on the C5-mode field (128^4 f32 reversible) some wave of
-  // every call passes the 1,666 words, so every call ran twice
-  // (ZFP_HIP_VERBOSE=1 shows it); a per-wave fallback is the missing piece.
-  // ZFP_HIP_PACK_WORDS=n turns it on with n staged words (tests, tuning).
+  // variable rate, f32/f64: the wave's segment (its 16 blocks, contiguous in
+  // the stream) staged back to back, sized for 16 worst-case blocks so every
+  // segment fits -- about the LDS of 16 padded slots, but the staging reads
+  // only the segment's words, where padded slots read 16 worst-case blocks'
+  // worth of words for every wave (128^4 f32 reversible decode 1.90 -> 1.46 ms).
+  // ZFP_HIP_PACK_WORDS=n stages n words instead (tests: a segment past n
+  // words sets the error flag and the launch is repeated with padded slots);
+  // ZFP_HIP_FULL_SLOTS=1 padded slots only.
   uint32_t packw = 0;
   if (!p.fixed && half && !getenv("ZFP_HIP_FULL_SLOTS")) {
+    packw = (uint32_t)((126ull + (uint64_t)kBlocks4PerWave * per_block) / 64 + 1);
     if (const char* e = getenv("ZFP_HIP_PACK_WORDS"))
       packw = (uint32_t)atoi(e);
-    if ((size_t)packw * 8 < xfull / 2 || packw >= kBlocks4PerWave * a.swp)
+    if ((size_t)packw * 8 < xfull / 2 || (size_t)kDec4HeadWords * 8 + (size_t)packw * 8 > 160 * 1024)
       packw = 0;
   }
   for (int attempt = 0; attempt < 2; attempt++) {

@@ -20,6 +20,7 @@ Additions (keyword-only, optional):
 import ctypes
 import itertools
 import os
+import threading
 
 import numpy as np
 
@@ -150,6 +151,36 @@ class ZfpBytes(bytes):
     block_index = None
 
 
+# Stream buffers as numpy arrays.  Output: a per-thread scratch buffer reused
+# across calls (fresh pages of a new buffer cost a page fault each while the
+# device-to-host copy fills them; the header and stream writers store whole
+# words, so its old contents never reach the result), copied once into the
+# returned bytes object.  Input: np.zeros takes calloc'd pages (zeroed by the
+# kernel, outside the GIL) where ctypes.create_string_buffer memsets under it.
+# zfp_parallel's worker threads otherwise serialise on these copies.
+_tls = threading.local()
+
+
+def _out_buffer(size):
+    a = getattr(_tls, "out", None)
+    if a is None or a.size < size:
+        a = np.empty(max(size, 1 << 20), dtype=np.uint8)
+        _tls.out = a
+    return a, a.ctypes.data
+
+
+def _stream_bytes(a, n):
+    return ZfpBytes(memoryview(a)[:n])
+
+
+def _in_buffer(compressed_data):
+    """The stream plus one spare zero word (the reader peeks a word past the end)."""
+    src = np.frombuffer(compressed_data, dtype=np.uint8)
+    a = np.zeros(src.size + 8, dtype=np.uint8)
+    a[:src.size] = src
+    return a, a.ctypes.data
+
+
 def _check_native(ret, what):
     if ret == 0:
         raise RuntimeError(what)
@@ -239,7 +270,7 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
             _lib.zfp_stream_set_hip_device(stream, device)
         _set_compression_mode(stream, type_none, ndim, tolerance, rate, precision)
         maxsize = _lib.zfp_stream_maximum_size(stream, field)
-        buf = ctypes.create_string_buffer(maxsize)
+        arr, buf = _out_buffer(maxsize)
         bstream = _lib.stream_open(buf, maxsize)
         _lib.zfp_stream_set_bit_stream(stream, bstream)
         _lib.zfp_stream_rewind(stream)
@@ -248,7 +279,7 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
         n = _lib.zfp_compress(stream, field)
         if n == 0:
             raise RuntimeError("Failed to write to stream")
-        out = ZfpBytes(ctypes.string_at(buf, n))
+        out = _stream_bytes(arr, n)
         out.block_index = _export_index(stream)
         return out
     finally:
@@ -277,8 +308,8 @@ def decompress_numpy(compressed_data, *, device=-1):
     """Decompress a stream written with a full header (pyx:533-557)."""
     if compressed_data is None:
         raise TypeError("compressed_data cannot be None")
-    data = bytes(compressed_data)
-    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    arr, buf = _in_buffer(compressed_data)
+    data = memoryview(arr)[:-8]
     field = _lib.zfp_field_alloc()
     bstream = _lib.stream_open(buf, len(data))
     stream = _lib.zfp_stream_open(bstream)
@@ -307,8 +338,8 @@ def _decompress(compressed_data, ztype, shape, out=None, tolerance=-1, rate=-1, 
         raise ValueError("User-provided shape has too many dimensions (up to 4 supported)")
     if len(shape) <= 0:
         raise ValueError("User-provided shape needs at least one dimension")
-    data = bytes(compressed_data)
-    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    arr, buf = _in_buffer(compressed_data)
+    data = memoryview(arr)[:-8]
     bstream = _lib.stream_open(buf, len(data))
     stream = _lib.zfp_stream_open(bstream)
     dtype = ztype_to_dtype(ztype)
@@ -345,8 +376,8 @@ def header(compressed_data):
     """Stream header as a dict (pyx:596-650; `expert.maxbits` reports minbits as the reference does)."""
     if compressed_data is None:
         raise TypeError("compressed_data cannot be None")
-    data = bytes(compressed_data)
-    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    arr, buf = _in_buffer(compressed_data)
+    data = memoryview(arr)[:-8]
     field = _lib.zfp_field_alloc()
     bstream = _lib.stream_open(buf, len(data))
     stream = _lib.zfp_stream_open(bstream)
@@ -468,7 +499,7 @@ def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1,
         _set_compression_mode(stream, type_none, chunkit.ndim, tolerance, rate, precision)
         ck = chunkit.chunk_ptr(ichunk)
         maxsize = _lib.zfp_stream_maximum_size_chunk(stream, field, ck) + (HEADER_MAX_BITS + 63) // 64 * 8 + 8
-        buf = ctypes.create_string_buffer(maxsize)
+        arr, buf = _out_buffer(maxsize)
         bstream = _lib.stream_open(buf, maxsize)
         _lib.zfp_stream_set_bit_stream(stream, bstream)
         _lib.zfp_stream_rewind(stream)
@@ -477,7 +508,7 @@ def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1,
         n = _lib.zfp_compress_chunk(stream, ck, field)
         if n == 0:
             raise RuntimeError("Failed to write to stream")
-        out = ZfpBytes(ctypes.string_at(buf, n))
+        out = _stream_bytes(arr, n)
         out.block_index = _export_index(stream)
         return out
     finally:
@@ -493,8 +524,8 @@ def decompress_numpy_portion(compressed_data, py_raw_array, chunkit, ichunk, *, 
     if compressed_data is None:
         raise TypeError("compressed_data cannot be None")
     field = _init_field_raw(py_raw_array, chunkit)
-    data = bytes(compressed_data)
-    buf = ctypes.create_string_buffer(data, len(data) + 8)
+    arr, buf = _in_buffer(compressed_data)
+    data = memoryview(arr)[:-8]
     bstream = _lib.stream_open(buf, len(data))
     stream = _lib.zfp_stream_open(bstream)
     idx = None

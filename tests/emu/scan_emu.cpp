@@ -35,13 +35,15 @@ struct Case {
 
 template <typename S, int DIMS, bool REV>
 static bool run_scan(const Case& c, const std::vector<uint64_t>& words, uint64_t g0, uint64_t nb,
-                     const std::vector<uint64_t>& truth, uint64_t seg_bits, uint32_t max_len, int* passes)
+                     const std::vector<uint64_t>& truth, uint64_t seg_bits, uint64_t lead, uint32_t max_len,
+                     int* passes)
 {
   ScanArgs a{};
   a.in = words.data();
   a.in_words = words.size();
   a.g0 = (uint32_t)g0;
   a.seg_bits = seg_bits;
+  a.lead = lead;
   const uint64_t avail = words.size() * 64 - g0;
   uint64_t extent = nb * (uint64_t)max_len;
   extent = extent < avail ? extent : avail;
@@ -170,11 +172,13 @@ static int run_case(const Case& c, std::mt19937_64& rng)
         }
       }
     }
-    for (uint64_t seg : {128ull, 2048ull, 1ull << 20}) {
-      int passes = 0;
-      if (!run_scan<S, DIMS, REV>(c, words, g0, nb, truth, seg, max_len, &passes))
-        fails++;
-    }
+    // lead-ins: none, shorter than a block, several segments
+    for (uint64_t seg : {128ull, 2048ull, 1ull << 20})
+      for (uint64_t lead : {(uint64_t)0, (uint64_t)300, 4 * seg + 77}) {
+        int passes = 0;
+        if (!run_scan<S, DIMS, REV>(c, words, g0, nb, truth, seg, lead, max_len, &passes))
+          fails++;
+      }
   }
   printf("%s %s\n", c.name, fails ? "FAIL" : "ok");
   return fails;

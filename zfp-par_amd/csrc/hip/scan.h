@@ -6,10 +6,13 @@
 // Parallel resynchronising parse.  The stream is cut into segments of L bits,
 // one lane per segment:
 //
-//   pass 1  lane s parses blocks from the segment's first bit as if a block
-//           started there (speculatively: only segment 0 starts at a real
-//           block) until it leaves the segment, marking every block start in
-//           a bitmap (1 bit per stream bit) and recording where it left, X[s].
+//   pass 1  lane s parses blocks from `lead` bits before the segment's first
+//           bit as if a block started there (speculatively: only bit 0 starts
+//           a real block), follows that chain into the segment and on until
+//           it leaves it, marking every block start inside the segment in a
+//           bitmap (1 bit per stream bit) and recording where it left, X[s].
+//           The lead-in lets the chain resynchronise with the true one before
+//           the segment starts, so that pass 2 usually confirms it at once.
 //   pass k  lane s re-parses from X[s-1], the exit of the chain of segment
 //           s-1.  Parsing is deterministic, so the moment this chain lands on
 //           a start already marked in segment s it coincides with segment s's
@@ -118,22 +121,48 @@ __device__ __forceinline__ void scan_section(R& rd, uint64_t& p, uint32_t& bits,
   }
   {
     // closed form: after the "1" test the section is tokens "0", "11", "10"
-    // and ends at the first run of ones of odd length (codec_dev.h)
-    const uint64_t S = w >> 1;
-    const uint64_t starts = S & ~(S << 1);
-    const uint64_t se = S + (starts & kEven), so = S + (starts & kOdd);
-    const uint64_t ends = (((se & ~S) & kOdd) | ((so & ~S) & kEven)) & ~(1ull << 63);
-    if (ends) {
-      const uint32_t q = ctz64(ends);
-      const uint64_t mq = (ends - 1) & ~ends;
-      const uint32_t ones = (uint32_t)__popcll(S & mq);
-      const uint32_t P = q - (ones - 1) / 2;
-      if (n + P <= (uint32_t)SIZE - 1 && q + 2 <= bits) {
-        p += q + 2;
-        bits -= q + 2;
-        n += P;
-        return;
+    // and ends at the first run of ones of odd length (codec_dev.h), taken
+    // one 64-bit window at a time: a window without an end holds only "0"
+    // and "11" tokens (every run of ones even) except a last run of ones
+    // reaching its top, whose odd "1" starts a token that the next window
+    // continues.  4D sections are often longer than one window; one window
+    // costs a peek, where the reference loop costs one per coefficient.
+    uint64_t S = w >> 1;   // token bits from stream bit q0
+    uint32_t avail = 63;   // of which the low `avail` are stream bits
+    uint64_t q0 = p + 1;
+    uint32_t used = 1, nn = n;  // bits (the "1" test) and coefficients so far
+    for (;;) {
+      const uint64_t real = low_mask(avail);
+      S &= real;
+      const uint64_t starts = S & ~(S << 1);
+      const uint64_t se = S + (starts & kEven), so = S + (starts & kOdd);
+      const uint64_t ends = (((se & ~S) & kOdd) | ((so & ~S) & kEven)) & real;
+      if (ends) {
+        const uint32_t q = ctz64(ends);
+        const uint64_t mq = (ends - 1) & ~ends;
+        const uint32_t ones = (uint32_t)__popcll(S & mq);
+        const uint32_t P = q - (ones - 1) / 2;
+        if (nn + P <= (uint32_t)SIZE - 1 && used + q + 1 <= bits) {
+          p = q0 + q + 1;
+          bits -= used + q + 1;
+          n = nn + P;
+          return;
+        }
+        break;
       }
+      // the run of ones at the window's top: an odd one leaves its last "1"
+      const uint64_t top = S << (64 - avail);  // avail >= 63
+      const uint32_t run = ~top ? (uint32_t)__builtin_clzll(~top) : 64u;
+      const uint32_t c = avail - (run & 1u);
+      const uint32_t ones = (uint32_t)__popcll(S & low_mask(c));  // even
+      const uint32_t cnt = c - ones / 2;  // "0" tokens + "11" tokens
+      if (nn + cnt > (uint32_t)SIZE - 1 || used + c > bits)
+        break;
+      nn += cnt;
+      used += c;
+      q0 += c;
+      S = rd.peek(q0);
+      avail = 64;
     }
   }
   // reference loop (long sections, the implicit last coefficient, budget cuts)
@@ -241,6 +270,7 @@ struct ScanArgs {
   uint32_t g0;
   uint32_t first;        // 1: pass 1 (bitmap is all zero; speculative starts)
   uint64_t seg_bits;     // L, a multiple of 64
+  uint64_t lead;         // pass 1: a segment's chain starts this many bits early
   uint64_t nseg;
   uint64_t limit;        // bits [0, limit) are scanned (limit = extent + 1)
   uint64_t* bm;          // boundary bitmap, ceil(limit / 64) words
@@ -263,14 +293,13 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
   if (s == 0)
     e = 0;
   else if (a.first)
-    e = lo;
+    e = lo > a.lead ? lo - a.lead : 0;  // lead-in start (0: the true chain)
   else
     e = a.xsnap[s - 1];
   if (!a.first) {
     if (e == a.entry_used[s])
       return;  // this segment's chain already starts where the previous one exits
   }
-  a.entry_used[s] = e;
   RingReader rd;
   rd.in = a.in;
   rd.in_words = a.in_words;
@@ -281,6 +310,19 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
   // a zero float block is the single bit "0" (integer blocks have no flag)
   const bool runs = !std::is_integral<S>::value && a.sp.minbits <= 1;
   uint64_t p = e;
+  // pass 1: the speculative chain starts `lead` bits before the segment and
+  // is only followed (nothing marked) until it enters it, so that it has
+  // usually met the true chain by then
+  while (p < lo) {
+    const uint64_t h = rd.peek(p);
+    if (runs && !(h & 1)) {
+      const uint64_t c = ctz64(h);
+      p += c < lo - p ? c : lo - p;
+      continue;
+    }
+    p += scan_block<S, DIMS, REV>(rd, p, a.sp);
+  }
+  a.entry_used[s] = p;
   uint64_t wi = lo >> 6;     // bitmap word being assembled
   uint64_t acc = 0;          // this chain's starts in word wi
   bool merged = false;

@@ -1057,6 +1057,19 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
 // ---------------------------------------------------------------------------
 // Index scan (scan.h): block starts of a variable-rate stream resident on the
 // device at d_in (word 0 holds bit g0 of the first block), written into `x`.
+// Segment length and pass-1 lead-in (ZFP_HIP_SCAN_SEG_BITS / _LEAD_BITS):
+// a speculative chain resynchronises after ~116-205 Kbit on average (DESIGN.md
+// §3.5); without a lead-in short segments cost one pass per segment of every
+// unsynchronised stretch.  With the lead-in nearly every segment is right after
+// pass 1, so the segments are kept short (more lanes, a shorter serial parse).
+#ifndef ZFP_SCAN_MIN_SEG_BITS
+#define ZFP_SCAN_MIN_SEG_BITS 16384
+#endif
+#ifndef ZFP_SCAN_LEAD_BITS
+#define ZFP_SCAN_LEAD_BITS 524288
+#endif
+constexpr uint64_t kScanMinSegBits = ZFP_SCAN_MIN_SEG_BITS, kScanLeadBits = ZFP_SCAN_LEAD_BITS;
+
 static uint64_t scan_seg_bits(uint64_t limit)
 {
   if (const char* e = getenv("ZFP_HIP_SCAN_SEG_BITS")) {
@@ -1064,14 +1077,19 @@ static uint64_t scan_seg_bits(uint64_t limit)
     if (v >= 64)
       return v & ~63ull;
   }
-  // about 2^18 lanes at most; segments of at least 64 Kbit: a speculative
-  // chain resynchronises after ~116-205 Kbit on average, so
-  // shorter segments cost more passes than their shorter parses save
-  // (512^3 f64 precision 32: 69 ms at 16 Kbit, 55 ms at 64 Kbit; 128^4 f32
-  // reversible: 378 -> 205 ms; profiles/r2d_scan_seg.txt)
+  // about 2^18 lanes at most
   uint64_t L = (limit + (1ull << 18) - 1) >> 18;
-  L = std::max<uint64_t>(L, 65536);
+  L = std::max<uint64_t>(L, kScanMinSegBits);
   return (L + 63) & ~63ull;
+}
+
+// pass-1 lead-in (scan.h): long enough that a speculative chain has almost
+// always met the true one before its segment starts
+static uint64_t scan_lead_bits()
+{
+  if (const char* e = getenv("ZFP_HIP_SCAN_LEAD_BITS"))
+    return strtoull(e, nullptr, 10);
+  return kScanLeadBits;
 }
 
 static void launch_scan_dispatch(Ctx* c, const Plan& p, const ScanArgs& a)
@@ -1111,6 +1129,7 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
   a.g0 = g0;
   a.first = 1;
   a.seg_bits = seg;
+  a.lead = scan_lead_bits();
   a.nseg = nseg;
   a.limit = limit;
   a.bm = bm;

@@ -81,6 +81,6 @@ def test_index_scan_matches_oracle_block_starts(oracle_obj):
     in precision, accuracy, reversible and expert modes, 3D and 4D, f32 and f64,
     at several segment sizes and unaligned stream offsets."""
     d, obj = oracle_obj
-    r = subprocess.run([_build(d, "scan_emu.cpp", [obj])], capture_output=True, text=True, timeout=600)
+    r = subprocess.run([_build(d, "scan_emu.cpp", [obj, "-DZFP_SCAN_RING_WORDS=4"])], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "scan mismatches 0" in r.stdout, r.stdout

@@ -28,9 +28,10 @@ def main():
     ap.add_argument("--mode", default="precision")
     ap.add_argument("--param", type=float, default=32)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default=os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so"))
     a = ap.parse_args()
     dtype = np.float64 if a.dtype == "f64" else np.float32
-    api = ZfpCAPI(os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so"))
+    api = ZfpCAPI(a.lib)
     api.enable_index()
     n = a.n
     shape = (n,) * a.dims
@@ -57,6 +58,9 @@ def main():
         t3 = time.perf_counter()
         scan = api.last_scan()
         same = out.tobytes() == ref.tobytes()
+        if a.mode == "reversible":  # lossless: both decodes must give the field back
+            same = "%s (index decode lossless %s, scan decode lossless %s)" % (
+                same, ref.tobytes() == arr.tobytes(), out.tobytes() == arr.tobytes())
         print("rep %d: stream %d B, with index %.1f ms (kernel %.3f ms), without %.1f ms: scan %.3f ms in %d passes, "
               "identical %s" % (r, len(data), 1e3 * (t1 - t0), km.value, 1e3 * (t3 - t2), scan[0], scan[1], same),
               flush=True)

@@ -44,7 +44,10 @@ namespace zfp_amd {
 
 // ---------------------------------------------------------------------------
 // per-lane stream reader: ring of kRing words in LDS + kHalf prefetched words
-constexpr uint32_t kRing = 16;
+#ifndef ZFP_SCAN_RING_WORDS
+#define ZFP_SCAN_RING_WORDS 16
+#endif
+constexpr uint32_t kRing = ZFP_SCAN_RING_WORDS;
 constexpr uint32_t kHalf = kRing / 2;
 
 struct RingReader {
@@ -76,6 +79,13 @@ struct RingReader {
   // make words i and i+1 resident (i >= base: positions only move forward)
   __device__ __forceinline__ void ensure(uint64_t i)
   {
+#ifdef EMU_KERNEL_BUILTINS
+    if (i < base) {  // host emulation: a read behind the ring (positions must only move forward)
+      fprintf(stderr, "RingReader: word %llu behind the ring base %llu\n", (unsigned long long)i,
+              (unsigned long long)base);
+      abort();
+    }
+#endif
     if (i + 1 < base + kRing)
       return;
     if (i + 1 >= base + kRing + kHalf) {  // jumped past the prefetched half
@@ -119,6 +129,8 @@ __device__ __forceinline__ void scan_section(R& rd, uint64_t& p, uint32_t& bits,
     bits--;
     return;
   }
+  uint64_t q0 = p + 1;        // stream bit of the current window's token bit 0
+  uint32_t used = 1, nn = n;  // bits (the "1" test) and coefficients before it
   {
     // closed form: after the "1" test the section is tokens "0", "11", "10"
     // and ends at the first run of ones of odd length (codec_dev.h), taken
@@ -129,8 +141,6 @@ __device__ __forceinline__ void scan_section(R& rd, uint64_t& p, uint32_t& bits,
     // costs a peek, where the reference loop costs one per coefficient.
     uint64_t S = w >> 1;   // token bits from stream bit q0
     uint32_t avail = 63;   // of which the low `avail` are stream bits
-    uint64_t q0 = p + 1;
-    uint32_t used = 1, nn = n;  // bits (the "1" test) and coefficients so far
     for (;;) {
       const uint64_t real = low_mask(avail);
       S &= real;
@@ -165,13 +175,22 @@ __device__ __forceinline__ void scan_section(R& rd, uint64_t& p, uint32_t& bits,
       avail = 64;
     }
   }
-  // reference loop (long sections, the implicit last coefficient, budget cuts)
-  while (bits && n < (uint32_t)SIZE) {
-    bits--;
-    const uint32_t t = (uint32_t)(rd.peek(p) & 1);
-    p++;
-    if (!t)
-      break;
+  // reference loop (the implicit last coefficient, budget cuts), entered where
+  // the windows stopped -- at a token boundary, past a "1" test (the ring
+  // reader only moves forward)
+  p = q0;
+  bits -= used;
+  n = nn;
+  for (bool inner = true;; inner = false) {
+    if (!inner) {
+      if (!(bits && n < (uint32_t)SIZE))
+        break;
+      bits--;
+      const uint32_t t = (uint32_t)(rd.peek(p) & 1);
+      p++;
+      if (!t)
+        break;
+    }
     uint32_t rem = (uint32_t)SIZE - 1 - n;
     rem = rem < bits ? rem : bits;
     for (;;) {

@@ -1059,14 +1059,17 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
 // device at d_in (word 0 holds bit g0 of the first block), written into `x`.
 // Segment length and pass-1 lead-in (ZFP_HIP_SCAN_SEG_BITS / _LEAD_BITS):
 // a speculative chain resynchronises after ~116-205 Kbit on average (DESIGN.md
-// §3.5); without a lead-in short segments cost one pass per segment of every
-// unsynchronised stretch.  With the lead-in nearly every segment is right after
-// pass 1, so the segments are kept short (more lanes, a shorter serial parse).
+// §3.5), so short segments cost one pass per segment of every unsynchronised
+// stretch.  A lead-in cuts the passes of f64 precision-32 streams (512^3: 18 ->
+// 5 at 128 Kbit segments and 512 Kbit lead-in, 45 -> 41 ms) but not of 4D
+// reversible ones, whose unsynchronised stretches run for megabits (128^4: 91
+// passes at 64 Kbit without, 42 at 128 Kbit with, 145 -> 236 ms), so it is off
+// by default (profiles/r3_scan_lead.txt).
 #ifndef ZFP_SCAN_MIN_SEG_BITS
-#define ZFP_SCAN_MIN_SEG_BITS 16384
+#define ZFP_SCAN_MIN_SEG_BITS 65536
 #endif
 #ifndef ZFP_SCAN_LEAD_BITS
-#define ZFP_SCAN_LEAD_BITS 524288
+#define ZFP_SCAN_LEAD_BITS 0
 #endif
 constexpr uint64_t kScanMinSegBits = ZFP_SCAN_MIN_SEG_BITS, kScanLeadBits = ZFP_SCAN_LEAD_BITS;
 

@@ -98,9 +98,16 @@ __device__ __forceinline__ uint32_t ctz64(uint64_t x)
 // land in spare words at the slot's end (sized by slot_words_for) that are
 // never read; readers mask at the block length.
 // ---------------------------------------------------------------------------
+// ZFP_EXP_PLAIN_STORE (timing experiments only, wrong output): plain stores in
+// place of the LDS ORs, to price the atomics
+#if ZFP_EXP_PLAIN_STORE
+#define ZFP_LDS_OR(p, v) (void)(*(p) = (v))
+#else
+#define ZFP_LDS_OR(p, v) (void)__hip_atomic_fetch_or((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)
+#endif
 __device__ __forceinline__ void lds_or32(uint32_t* p, uint32_t v)
 {
-  __hip_atomic_fetch_or(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+  ZFP_LDS_OR(p, v);
 }
 
 // Writes are dword-granular funnel shifts (v_alignbit_b32: one full-rate op per
@@ -829,22 +836,17 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
 __device__ __forceinline__ void fr_write32(int32_t Q, uint32_t v)
 {
   const uint32_t a = ~(((uint32_t)(Q >> 3)) | 3u);
-  __hip_atomic_fetch_or(lds_at(a), __builtin_amdgcn_alignbit(v, 0u, (uint32_t)Q), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_WAVEFRONT);
-  __hip_atomic_fetch_or(lds_at(a + 4u), __builtin_amdgcn_alignbit(0u, v, (uint32_t)Q), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+  ZFP_LDS_OR(lds_at(a), __builtin_amdgcn_alignbit(v, 0u, (uint32_t)Q));
+  ZFP_LDS_OR(lds_at(a + 4u), __builtin_amdgcn_alignbit(0u, v, (uint32_t)Q));
 }
 
 // v1:v0 at bit address -Q: three dwords
 __device__ __forceinline__ void fr_write64(int32_t Q, uint32_t v0, uint32_t v1)
 {
   const uint32_t a = ~(((uint32_t)(Q >> 3)) | 3u);
-  __hip_atomic_fetch_or(lds_at(a), __builtin_amdgcn_alignbit(v0, 0u, (uint32_t)Q), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_WAVEFRONT);
-  __hip_atomic_fetch_or(lds_at(a + 4u), __builtin_amdgcn_alignbit(v1, v0, (uint32_t)Q), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_WAVEFRONT);
-  __hip_atomic_fetch_or(lds_at(a + 8u), __builtin_amdgcn_alignbit(0u, v1, (uint32_t)Q), __ATOMIC_RELAXED,
-                        __HIP_MEMORY_SCOPE_WAVEFRONT);
+  ZFP_LDS_OR(lds_at(a), __builtin_amdgcn_alignbit(v0, 0u, (uint32_t)Q));
+  ZFP_LDS_OR(lds_at(a + 4u), __builtin_amdgcn_alignbit(v1, v0, (uint32_t)Q));
+  ZFP_LDS_OR(lds_at(a + 8u), __builtin_amdgcn_alignbit(0u, v1, (uint32_t)Q));
 }
 
 #ifndef ZFP_FR32

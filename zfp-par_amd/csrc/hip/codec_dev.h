@@ -1059,8 +1059,15 @@ __device__ __forceinline__ uint32_t squeeze32(const uint32_t* sq, uint32_t f)
 // section is parsed in closed form and its consumption selected); only lanes
 // whose section is not closed-form run the reference loop, in a wave-uniform
 // branch.
+// ZFP_DP64_NOINLINE (experiment): one out-of-line copy instead of one per
+// unrolled plane, against the decoder's instruction-cache misses
+#if ZFP_DP64_NOINLINE
+#define ZFP_DP64_ATTR __attribute__((noinline))
+#else
+#define ZFP_DP64_ATTR __forceinline__
+#endif
 template <bool IMP = true, int SIZE = 64>
-__device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
+__device__ ZFP_DP64_ATTR uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
 {
   const uint32_t m = n < bits ? n : bits;
   uint32_t pos = r.pos;

@@ -68,6 +68,9 @@ def parse_args(argv=None):
     ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c2")
     ap.add_argument("--n", type=int, default=N, help="c2: edge of the per-GPU cube (default 1024)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--clock-warm-ms", type=float, default=250.0,
+                    help="untimed steps for at least this long before the W warmup steps: a cold MI355X needs "
+                         "about 20 ms of work to reach its steady clock (DESIGN.md 3.4), more than W=5 C2 steps")
     ap.add_argument("--dry-run", action="store_true", help="CPU/gloo plumbing check, no GPU")
     return ap.parse_args(argv)
 
@@ -280,6 +283,14 @@ def main():
         return nb
 
     nbytes = 0
+    # clock warm-up (untimed, like the warmup steps): steady-clock throughput
+    warm_launches = 0
+    tw = time.perf_counter()
+    while (time.perf_counter() - tw) * 1e3 < args.clock_warm_ms:
+        step()
+        warm_launches += 1
+        if warm_launches % 8 == 0:
+            torch.cuda.synchronize()
     for _ in range(args.warmup):
         nbytes = step()
     if distributed:
@@ -375,6 +386,7 @@ def main():
             "decode_kernel_ms": round(float(np.mean(dkms)), 4) if dkms else None,
             "decode_GBps": round(nvals * es / (np.mean(dms) * 1e-3) / 1e9, 2) if dms else None,
             "gather": gather,
+            "clock_warmup": {"ms": args.clock_warm_ms, "launches": warm_launches},
         }
         result.update(roundtrip)
         if not args.no_cpu and world == 1 and args.workload != "c4":

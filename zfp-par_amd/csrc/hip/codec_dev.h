@@ -1181,6 +1181,11 @@ __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_
 #ifndef ZFP_DEC32
 #define ZFP_DEC32 1
 #endif
+// ZFP_DEC32_SWITCH (experiment): leave the 32-bit body at the first plane with
+// a slow lane instead of running decode_plane64 for that lane inline
+#ifndef ZFP_DEC32_SWITCH
+#define ZFP_DEC32_SWITCH 0
+#endif
 // more lanes than this in a plane's slow path: the rest of the block without the 32-bit body
 #ifndef ZFP_DEC32_DENSE
 #define ZFP_DEC32_DENSE 16
@@ -1231,12 +1236,22 @@ __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_
     const uint32_t xx = squeeze32(sq, F);
     const uint32_t x = ubfe(lo, 0u, n) | (xx << n);
     const uint32_t used = n + (one ? q + 2u : 1u);
+#if ZFP_DEC32_SWITCH
+    // no decode_plane64 inside this loop (half the decoder's code): the first
+    // plane some lane cannot take here goes, with the rest, to the loop below
+    if (__builtin_amdgcn_ballot_w64(act && !fast) != 0) {
+      m32 = false;
+      ksw = k;
+      continue;
+    }
+#endif
     if (fast) {
       P[k] = x;
       r.pos += used;
       bits -= used;
       n += one ? np : 0u;
     }
+#if !ZFP_DEC32_SWITCH
     const bool slow = act && !fast;
     const uint64_t sm = __builtin_amdgcn_ballot_w64(slow);
     if (sm != 0) {
@@ -1252,6 +1267,7 @@ __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_
         ksw = k - 1;
       }
     }
+#endif
   }
   if (!m32) {
 #pragma unroll

@@ -89,7 +89,15 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   uint32_t* wslot = ldsw + (size_t)wv * 64 * sdw;
-  const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+#if ZFP_EXP_XCD_REMAP
+  // experiment: workgroup i runs on XCD i % 8; give each XCD a contiguous
+  // eighth of the field
+  const uint32_t nwg = gridDim.x;
+  const uint32_t bid = (nwg & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (nwg >> 3) + (blockIdx.x >> 3);
+#else
+  const uint32_t bid = blockIdx.x;
+#endif
+  const uint64_t w = (uint64_t)bid * kWavesPerGroup + wv;
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
   // the block loads are in flight while the wave copies the coder tables from

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--nparts", type=int, default=8)
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--profile", action="store_true", help="per-chunk time split of the last compress")
     a = ap.parse_args()
     from zfpy._zfp_par import zfp_p
     zp = zfp_p(tuple(a.shape), "float32", nparts=a.nparts)
@@ -46,11 +47,63 @@ def main():
         t0 = time.perf_counter()
         zp.decompress(nthreads=a.threads)
         td.append(time.perf_counter() - t0)
+    if a.profile:
+        profile_compress(zp, a)
     err = float(np.abs(arr - ref).max())
     nbytes = sum(len(d) for d in data)
     print("zfp_parallel shape %s rate %g nparts %d threads %d chunks %d: stream %d B, compress %.2f GB/s (best %.3f s), "
           "decompress %.2f GB/s (best %.3f s), max abs err %.3g"
           % (a.shape, a.rate, a.nparts, a.threads, len(data), nbytes, gb / min(tc), min(tc), gb / min(td), min(td), err))
+
+
+def profile_compress(zp, a):
+    """Wall time of each compress_numpy_portion split into its native call, the
+    stream copy into bytes and the index export (zfpy_c, timing wrappers)."""
+    import threading
+    from zfpy import zfpy_c
+    lock = threading.Lock()
+    rec = {}
+
+    def timed(name, fn):
+        def w(*x, **k):
+            t0 = time.perf_counter()
+            try:
+                return fn(*x, **k)
+            finally:
+                with lock:
+                    rec.setdefault(name, []).append((t0, time.perf_counter()))
+        return w
+
+    class Lib:
+        def __init__(self, lib):
+            self._l = lib
+
+        def __getattr__(self, nm):
+            f = getattr(self._l, nm)
+            return timed(nm, f) if nm in ("zfp_compress_chunk", "zfp_write_header", "stream_open") else f
+
+    saved = (zfpy_c._lib, zfpy_c._stream_bytes, zfpy_c._export_index, zfpy_c.compress_numpy_portion)
+    zfpy_c._lib = Lib(saved[0])
+    zfpy_c._stream_bytes = timed("stream_bytes", saved[1])
+    zfpy_c._export_index = timed("export_index", saved[2])
+    zfpy_c.compress_numpy_portion = timed("portion", saved[3])
+    import zfpy._zfp_par as zpar
+    saved_p = getattr(zpar, "compress_numpy_portion", None)
+    if saved_p is not None:
+        zpar.compress_numpy_portion = zfpy_c.compress_numpy_portion
+    try:
+        t0 = time.perf_counter()
+        zp.compress(nthreads=a.threads, rate=a.rate)
+        t1 = time.perf_counter()
+    finally:
+        zfpy_c._lib, zfpy_c._stream_bytes, zfpy_c._export_index, zfpy_c.compress_numpy_portion = saved
+        if saved_p is not None:
+            zpar.compress_numpy_portion = saved_p
+    print("profile: compress wall %.1f ms" % (1e3 * (t1 - t0)))
+    for nm, v in sorted(rec.items()):
+        d = [1e3 * (b - x) for x, b in v]
+        print("  %-20s n=%d  sum %.1f ms  max %.1f ms  first start +%.1f ms  last end +%.1f ms"
+              % (nm, len(v), sum(d), max(d), 1e3 * (min(x for x, _ in v) - t0), 1e3 * (max(b for _, b in v) - t0)))
 
 
 if __name__ == "__main__":

@@ -180,8 +180,9 @@ class ZfpCAPI:
             self.last_index = idx
 
     def compress(self, arr, mode, param=None, ztype=None, header=False, chunk=None, strided=False,
-                 execution=None):
-        """Returns the compressed bytes exactly as zfp_compress leaves them."""
+                 execution=None, pad_bits=0):
+        """Returns the compressed bytes exactly as zfp_compress leaves them (after
+        `pad_bits` zero bits, written with stream_pad, when given)."""
         if ztype is None:
             ztype = TYPE_OF[arr.dtype]
         field = self.field_for(arr, strided)
@@ -196,6 +197,8 @@ class ZfpCAPI:
         self.lib.zfp_stream_rewind(zs)
         if header:
             assert self.lib.zfp_write_header(zs, field, ZFP_HEADER_FULL)
+        if pad_bits:
+            self.lib.stream_pad(bs, pad_bits)
         if chunk is None:
             n = self.lib.zfp_compress(zs, field)
         else:

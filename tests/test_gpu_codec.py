@@ -122,6 +122,22 @@ def test_header_offset_stream_matches_oracle(product, oracle, mode, param):
     assert out.tobytes() == ref.tobytes()
 
 
+@pytest.mark.parametrize("pad", [1, 32, 64, 96, 100, 160, 255])
+@pytest.mark.parametrize("dtype,mode,param", [(np.float32, "rate", 8), (np.float32, "rate", 16),
+                                              (np.float64, "rate", 16), (np.float32, "rate", 12)])
+def test_bit_offset_stream_matches_oracle(product, oracle, pad, dtype, mode, param):
+    """Fixed-rate streams that start at any bit (the aligned encoder's copy-out
+    funnel-shifts its run; 16-byte stores pair the out words by their address)."""
+    rng = np.random.default_rng(pad)
+    a = rng.standard_normal((21, 26, 72)).astype(dtype)
+    got = product.compress(a, mode, param, pad_bits=pad)
+    params = _params(mode, param, TYPE_FLOAT if dtype == np.float32 else TYPE_DOUBLE, 3)
+    ow, end = oracle.compress_words(a, params, bit_offset=pad)
+    words = np.frombuffer(got + bytes((-len(got)) % 8), dtype=np.uint64)
+    assert words[: len(ow)].tobytes() == ow.tobytes()
+    assert len(got) == (end + 63) // 64 * 8
+
+
 @pytest.mark.parametrize("box", [[(0, 24), (0, 20), (8, 16)], [(8, 24), (4, 12), (0, 18)], [(4, 21), (0, 20), (16, 18)]])
 @pytest.mark.parametrize("mode,param", [("rate", 8), ("precision", 16)])
 def test_chunk_boxes_match_oracle(product, oracle, box, mode, param):

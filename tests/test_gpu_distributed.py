@@ -40,7 +40,7 @@ def _worker(rank, world, port, backend, kw, q):
         zp = zfpy.zfp_parallel(SHAPE, "float32", nparts=8)
         zp.get_numpy_array()[...] = _field()
         out = zdist.compress_distributed(zp, **kw)
-        q.put([(bytes(s), s.block_index) for s in out] if rank == 0 else None)
+        q.put([(bytes(s), getattr(s, "block_index", None)) for s in out] if rank == 0 else None)
     finally:
         dist.destroy_process_group()
 

@@ -190,3 +190,45 @@ def test_scan_matches_encoder_index_at_scale(product, oracle):
     assert with_idx.tobytes() == no_idx.tobytes()
     ms, passes = product.last_scan()
     print("256^3 f64 precision 32: %d B, scan %.3f ms, %d passes" % (len(data), ms, passes))
+
+
+def _field4(n, dtype):
+    """The C5-mode 4D field at n^4 (tools/kprof.py field4): F1 + .25 cos(.04 w)."""
+    x = np.arange(n, dtype=np.float64)
+    base = np.sin(0.05 * x)[None, :] * np.cos(0.03 * x)[:, None]
+    xy = 0.01 * x[None, :] * x[:, None] / n
+    f3 = base[None] + 0.5 * np.sin(0.02 * x[:, None, None] + xy[None])
+    return np.stack([(f3 + 0.25 * np.cos(0.04 * w)).astype(dtype) for w in range(n)])
+
+
+@pytest.mark.parametrize("n,dtype,mode,param,params", [
+    (64, np.float32, "reversible", None, params_reversible()),
+    (48, np.float64, "precision", 32, params_precision(32)),
+])
+def test_scan_4d_at_scale_matches_index_and_oracle(product, oracle, n, dtype, mode, param, params):
+    """Regression guard for the round-3 4D scan bug (a long group section's
+    reference-loop fallback restarted behind the forward-only ring reader, so
+    large 4D streams were indexed wrongly): a 4D stream of tens of megabytes is
+    decoded once with the encoder's index and once with none (the scan); both
+    equal the oracle's decode, and the second call really scanned
+    (src/template/decompress.c:105-140 is the serial walk this replaces)."""
+    arr = _field4(n, dtype)
+    data = product.compress(arr, mode, param)
+    idx = product.last_index
+    assert idx
+    with_idx, n1 = product.decompress(data, arr.shape, dtype, mode, param, index=idx)
+    product.lib.zfp_hip_index_free(idx)
+    product.last_index = None
+    assert product.last_scan() is None, "a matching encoder index must not be rescanned"
+    no_idx, n2 = product.decompress(data, arr.shape, dtype, mode, param)
+    scan = product.last_scan()
+    assert scan is not None, "a stream without an index must be scanned"
+    assert n1 == n2 == len(data)
+    want, end = _oracle_decode(oracle, data, arr.shape, dtype, params)
+    assert n1 == (end + 63) // 64 * 8
+    assert with_idx.tobytes() == want.tobytes()
+    assert no_idx.tobytes() == want.tobytes()
+    if mode == "reversible":
+        assert no_idx.tobytes() == arr.tobytes()
+    print("%d^4 %s %s: %d B stream, scan %.3f ms in %d passes" % (n, np.dtype(dtype).name, mode, len(data),
+                                                                 scan[0], scan[1]))

@@ -102,27 +102,34 @@ def test_rank_chunks_cover_every_chunk_once():
             assert owned == list(range(n))
 
 
-def _gather_worker(rank, world, port, nchunks, q):
+def _gather_worker(rank, world, port, nchunks, q, sub):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
+        # sub: the gather runs on the subgroup of global ranks 1..world-1 (its
+        # rank 0 is global rank 1): point-to-point peers must be global ranks
+        group = dist.new_group(list(range(1, world))) if sub else None
+        if sub and rank == 0:
+            q.put(None)
+            return
+        grank, gworld = dist.get_rank(group), dist.get_world_size(group)
         local = {}
-        for i in zdist.rank_chunks(nchunks, world, rank):
+        for i in zdist.rank_chunks(nchunks, gworld, grank):
             local[i] = zfpy.zfpy_c.ZfpBytes(bytes([i % 251]) * (100 + 37 * i))
             if i % 2:  # variable-rate chunks carry their block index
                 local[i].block_index = bytes([(7 * i) % 256]) * (50 + i)
-        out = zdist.gather_streams(local, nchunks, dst=0)
-        if rank == 0:
-            q.put([(bytes(s), s.block_index) for s in out])
+        out = zdist.gather_streams(local, nchunks, dst=0, group=group)
+        if grank == 0:
+            q.put([(bytes(s), getattr(s, "block_index", None), type(s) is bytes) for s in out])
         else:
             q.put(out)
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_gather_streams_gloo(world):
+@pytest.mark.parametrize("world,sub", [(2, False), (3, False), (3, True)])
+def test_gather_streams_gloo(world, sub):
     import multiprocessing as mp
     import socket
     with socket.socket() as sk:
@@ -131,7 +138,7 @@ def test_gather_streams_gloo(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     nchunks = 9
-    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, nchunks, q)) for r in range(world)]
+    ps = [ctx.Process(target=_gather_worker, args=(r, world, port, nchunks, q, sub)) for r in range(world)]
     for p in ps:
         p.start()
     res = [q.get(timeout=120) for _ in ps]
@@ -142,9 +149,10 @@ def test_gather_streams_gloo(world):
     assert len(root) == 1 and res.count(None) == world - 1
     got = root[0]
     assert len(got) == nchunks
-    for i, (s, blob) in enumerate(got):
+    for i, (s, blob, plain) in enumerate(got):
         assert s == bytes([i % 251]) * (100 + 37 * i)
         assert blob == (bytes([(7 * i) % 256]) * (50 + i) if i % 2 else None)
+        assert plain == (i % 2 == 0)  # chunks without an index come back as plain bytes
 
 
 # ---------------- CPU: header() ----------------

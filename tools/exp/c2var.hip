@@ -8,6 +8,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <string>
 #include "kernels3.h"
 using namespace zfp_amd;
 
@@ -94,6 +95,63 @@ __global__ __launch_bounds__(256, 3) void enc_stage(const float* __restrict__ da
   }
 }
 
+// round 4: the product kernel with the block loads of a workgroup's waves
+// staggered -- wave wv issues its loads once waves < wv/G*G have theirs in
+// registers (G waves load together); fewer bytes in flight per CU and the
+// waves' coder phases spread apart.
+template <int G, bool SYNC = true, bool WAIT0 = true>
+__global__ __launch_bounds__(256, 3) void enc_gate(const float* __restrict__ data, Geometry g, CodecParams cp,
+                                                 uint64_t* __restrict__ out, uint32_t sw, uint32_t sdw, uint32_t magic_c)
+{
+  __shared__ uint32_t lut[512];
+  __shared__ uint32_t gate;
+  extern __shared__ uint32_t ldsw[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint32_t* wslot = ldsw + (size_t)wv * 64 * sdw;
+  const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  const uint64_t first = w * 64;
+  const uint64_t b = first + lane;
+  if (threadIdx.x == 0) gate = 0;
+  if (SYNC) __syncthreads();
+  float v[64];
+  BlockPos p = block_pos(g, b, 3);
+  const uint32_t need = (uint32_t)(wv / G) * G;
+  if (need) {
+    while (__hip_atomic_load(&gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need)
+      __builtin_amdgcn_s_sleep(2);
+  }
+  gather3<float, true>(v, data, g, p);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&kCoderTables);
+    uint4* dst = reinterpret_cast<uint4*>(lut);
+    dst[lane] = src[lane];
+    dst[lane + 64] = src[lane + 64];
+    uint4* z = reinterpret_cast<uint4*>(wslot);
+    for (uint32_t i = lane; i < 16 * sdw; i += 64)
+      z[i] = make_uint4(0, 0, 0, 0);
+  }
+  if (WAIT0) {
+    __builtin_amdgcn_s_waitcnt(0);  // the block is in registers
+    if (lane == 0) __hip_atomic_fetch_add(&gate, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+  }
+  __builtin_amdgcn_wave_barrier();
+  OrSlot os{reinterpret_cast<uint64_t*>(wslot + (size_t)lane * sdw), sdw - 1};
+  encode_block3<float, false, true>(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  const uint32_t hw = sw >> 1, chunks = 64 * hw;
+  uint64_t* dst = out + first * sw;
+  for (uint32_t c = lane; c < chunks; c += 64) {
+    const uint32_t l = div_magic(c, magic_c);
+    const uint32_t* s = wslot + (size_t)l * sdw + 4 * (c - l * hw);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u4{s[0], s[1], s[2], s[3]}, reinterpret_cast<u4*>(dst + 2 * c));
+  }
+}
+
 template <typename K>
 static float time_it(K launch, int reps)
 {
@@ -134,6 +192,11 @@ int main(int argc, char** argv)
     hipLaunchKernelGGL((encode3_aligned<float, true, false>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_w, magic_c, 0u,
                        (Partial*)nullptr);
   };
+  if (argc > 1 && std::string(argv[1]) == "pmc") {  // a few launches for counter passes
+    for (int r = 0; r < 5; r++) full();
+    CK(hipDeviceSynchronize());
+    return 0;
+  }
   for (int r = 0; r < 3; r++) {
     float t = time_it(full, 20);
     printf("%-10s full      %.4f ms  %.0f GB/s(alg)  frac %.4f\n", tag, t, gb / t * 1e3, gb / t * 1e3 / 8000.0);
@@ -144,6 +207,42 @@ int main(int argc, char** argv)
   unsigned long long h = 0;
   CK(hipMemcpy(&h, cs, 8, hipMemcpyDeviceToHost));
   printf("%-10s checksum %016llx\n", tag, h);
+  for (int r = 0; r < 2; r++) {
+    float t;
+    t = time_it([&] { hipLaunchKernelGGL(enc_gate<1>, grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s gate1     %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL(enc_gate<2>, grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s gate2     %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL(enc_gate<4>, grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s gate4     %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((enc_gate<4, false, true>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s nosync-w0 %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((enc_gate<4, true, false>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s sync-lazy %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((enc_gate<4, false, false>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s nosync-lazy %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+  }
+  for (int r = 0; r < 2; r++) {
+    float t;
+    t = time_it([&] { hipLaunchKernelGGL((encode3_aligned<float, true, false, 2>), dim3((unsigned)(g.nblocks / 128)), dim3(128),
+                                         2 * 64 * sdw * 4, 0, d, g, cp, o, sw, sdw, magic_w, magic_c, 0u, (Partial*)nullptr); }, 20);
+    printf("%-10s wpg2      %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((encode3_aligned<float, true, false, 1>), dim3((unsigned)(g.nblocks / 64)), dim3(64),
+                                         1 * 64 * sdw * 4, 0, d, g, cp, o, sw, sdw, magic_w, magic_c, 0u, (Partial*)nullptr); }, 20);
+    printf("%-10s wpg1      %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((encode3_aligned<float, true, false, 8>), dim3((unsigned)(g.nblocks / 512)), dim3(512),
+                                         8 * 64 * sdw * 4, 0, d, g, cp, o, sw, sdw, magic_w, magic_c, 0u, (Partial*)nullptr); }, 20);
+    printf("%-10s wpg8      %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+  }
+  for (int G : {1, 2}) {
+    CK(hipMemset(cs, 0, 8));
+    if (G == 1) hipLaunchKernelGGL(enc_gate<1>, grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c);
+    else hipLaunchKernelGGL(enc_gate<2>, grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c);
+    hipLaunchKernelGGL(checksum, dim3(1024), dim3(256), 0, 0, o, (uint64_t)(N / 4), cs);
+    unsigned long long h2 = 0;
+    CK(hipMemcpy(&h2, cs, 8, hipMemcpyDeviceToHost));
+    printf("%-10s gate%d checksum %016llx\n", tag, G, h2);
+  }
   if (stages) {
     float t;
     t = time_it([&] { hipLaunchKernelGGL(enc_stage<1>, grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);

@@ -10,7 +10,7 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "run_counter_collection.csv"))):
         agg[short][(r["Dispatch_Id"], r["Counter_Name"])].append(float(r["Counter_Value"]))
 out = {}
 for k, m in agg.items():
-    if "zfp" not in k and "encode" not in k and "decode" not in k:
+    if "zfp" not in k and "encode" not in k and "decode" not in k and "enc_" not in k:
         continue
     per = collections.defaultdict(list)
     for (disp, name), vals in m.items():

@@ -78,8 +78,8 @@ __host__ __device__ constexpr uint32_t slot_dwords_for(uint32_t lim) { return (l
 #define ZFP_ENC_PRIO_OUT 0
 #endif
 
-template <typename S, bool VEC, bool REV>
-__global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
+template <typename S, bool VEC, bool REV, int WPG = kWavesPerGroup>
+__global__ __launch_bounds__(64 * WPG, 3) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
                                                        uint64_t* __restrict__ out, uint32_t sw, uint32_t sdw,
                                                        uint32_t magic_w, uint32_t magic_c, uint32_t r0,
                                                        Partial* __restrict__ partials)
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
 #else
   const uint32_t bid = blockIdx.x;
 #endif
-  const uint64_t w = (uint64_t)bid * kWavesPerGroup + wv;
+  const uint64_t w = (uint64_t)bid * WPG + wv;
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
   // the block loads are in flight while the wave copies the coder tables from
@@ -167,7 +167,67 @@ __global__ __launch_bounds__(256, 3) void encode3_aligned(const S* __restrict__ 
     }
     return;
   }
-  // run words j = 0..total-1 land at bit r0 + 64 j of out[first*sw ...]
+  // run words j = 0..total-1 land at bit r0 + 64 j of out[first*sw ...]: out
+  // word o (o = 0..total) holds bits of run words o-1 and o; words 0 and total
+  // are shared with the neighbouring waves (partials).
+  if ((sw & 1) == 0) {
+    // 16-byte stores of out-word pairs aligned in memory: (o0 + 2c, o0 + 2c + 1)
+    // with o0 = 1 when dst is 8 (mod 16).  In dwords, with D the run's dwords
+    // and j = ceil(r0 / 32), out dword k = alignbit(D[k-j+1], D[k-j], 32j - r0).
+    // A pair reads its chunk's four run dwords (one slot) and the neighbouring
+    // run word: the previous one (o0 = 0) or the next one (o0 = 1).
+    const uint32_t hw = sw >> 1, chunks = (uint32_t)nb * hw;
+    const uint32_t jj = (r0 + 31u) >> 5, sh = 32u * jj - r0;
+    const uint32_t o0 = (uint32_t)(reinterpret_cast<uintptr_t>(dst) >> 3) & 1u;
+    for (uint32_t c = lane; c < chunks; c += 64) {
+      const uint32_t l = div_magic(c, magic_c), cs = c - l * hw;
+      const uint32_t* s = wslot + (size_t)l * sdw + 4 * cs;
+      uint32_t X[6];
+      if (o0 == 0) {
+        // run word 2c - 1: the previous chunk's, or the last word of slot l - 1
+        const uint32_t* q = cs ? s - 2 : wslot + (size_t)(l ? l - 1 : 0) * sdw + 2 * sw - 2;
+        X[0] = c ? q[0] : 0u;
+        X[1] = c ? q[1] : 0u;
+        X[2] = s[0], X[3] = s[1], X[4] = s[2], X[5] = s[3];
+      } else {
+        // run word 2c + 2: the next chunk's, or the first word of slot l + 1
+        const bool in_run = 2 * c + 2 < total;
+        const uint32_t* q = cs + 1 < hw ? s + 4 : wslot + (size_t)(in_run ? l + 1 : l) * sdw;
+        X[0] = s[0], X[1] = s[1], X[2] = s[2], X[3] = s[3];
+        X[4] = in_run ? q[0] : 0u;
+        X[5] = in_run ? q[1] : 0u;
+      }
+      // out dwords 2 o0 + 4c + i, i = 0..3 (X[0] is run dword 2 o0 + 4c - 2)
+      uint32_t y[4];
+#pragma unroll
+      for (int i = 0; i < 4; i++)
+        y[i] = jj == 1 ? __builtin_amdgcn_alignbit(X[i + 2], X[i + 1], sh) : __builtin_amdgcn_alignbit(X[i + 1], X[i], sh);
+      const uint32_t o = o0 + 2 * c;  // first out word of the pair
+      const uint64_t v0 = ((uint64_t)y[1] << 32) | y[0], v1 = ((uint64_t)y[3] << 32) | y[2];
+      if (o == 0) {
+        partials[2 * w] = Partial{first * sw, v0};
+        dst[1] = v1;
+      } else if (o + 1 == total) {
+        dst[o] = v0;
+        partials[2 * w + 1] = Partial{first * sw + total, v1};
+      } else {
+#if ZFP_NT_STORE && defined(__HIP_DEVICE_COMPILE__)
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u4{y[0], y[1], y[2], y[3]}, reinterpret_cast<u4*>(dst + o));
+#else
+        *reinterpret_cast<uint4*>(dst + o) = make_uint4(y[0], y[1], y[2], y[3]);
+#endif
+      }
+    }
+    if (lane == 0) {
+      // the word no pair covers: the tail (o0 = 0) or the head (o0 = 1)
+      if (o0 == 0)
+        partials[2 * w + 1] = Partial{first * sw + total, run_word(total - 1) >> (64 - r0)};
+      else
+        partials[2 * w] = Partial{first * sw, run_word(0) << r0};
+    }
+    return;
+  }
   for (uint32_t j = lane; j <= total; j += 64) {
     const uint64_t cur = j < total ? run_word(j) : 0ull;
     const uint64_t prev = j > 0 ? run_word(j - 1) : 0ull;

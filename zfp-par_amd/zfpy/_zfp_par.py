@@ -21,7 +21,7 @@ from multiprocessing.sharedctypes import RawArray
 
 import numpy as np
 
-from .zfpy_c import compress_numpy_portion, decompress_numpy_portion, device_count, zfp_chunkit
+from .zfpy_c import _compress_portion, _decompress_portion, device_count, zfp_chunkit
 
 _TYPECODE = {"float32": "f", "float64": "d", "int32": "i", "int64": "q"}
 _ITEMSIZE = {"float32": 4, "float64": 8, "int32": 4, "int64": 8}
@@ -55,6 +55,7 @@ class zfp_p:
         self._np_array = np.frombuffer(self._raw_arr, dtype=dtype).reshape(shape)
         self._chunkit = zfp_chunkit(self._np_array, chunks_per_block, method)
         self._compress_data = []
+        self._index_of = []  # (stream object, block-index blob) per chunk of the last compress()
         ndev = device_count()
         self._ngpus = max(1, min(ngpus or 1, ndev if ndev > 0 else 1))
 
@@ -73,16 +74,21 @@ class zfp_p:
         return ichunk % self._ngpus if self._ngpus > 1 else -1
 
     def compress(self, nthreads=-1, tolerance=-1, rate=-1, precision=-1):
-        """Compress every chunk; result kept in self._compress_data (list of bytes, one per chunk)."""
+        """Compress every chunk; result kept in self._compress_data (list of bytes, one per chunk).
+        Chunk streams are plain bytes (as the reference's); a variable-rate chunk's GPU block index
+        is kept beside its stream and used by decompress() while that stream object is the one
+        compress() returned."""
         if nthreads == -1:
             nthreads = cpu_count()
         tasks = [(i, tolerance, rate, precision) for i in range(self._chunkit.get_nchunks())]
 
         def one(i, tol, r, p):
-            return compress_numpy_portion(self._raw_arr, self._chunkit, i, tol, r, p, device=self._device_of(i))
+            return _compress_portion(self._raw_arr, self._chunkit, i, tol, r, p, True, self._device_of(i), True)
 
         with ThreadPool(processes=max(1, min(nthreads, len(tasks) or 1))) as pool:
-            self._compress_data = pool.starmap(one, tasks)
+            res = pool.starmap(one, tasks)
+        self._compress_data = [d for d, _ in res]
+        self._index_of = [(d, blob) for d, blob in res]
         return self._compress_data
 
     def decompress(self, nthreads=-1):
@@ -94,7 +100,10 @@ class zfp_p:
             raise RuntimeError("no compressed data for this partition (call compress first)")
 
         def one(i):
-            decompress_numpy_portion(data[i], self._np_array, self._chunkit, i, device=self._device_of(i))
+            blob = getattr(data[i], "block_index", None)
+            if blob is None and i < len(self._index_of) and self._index_of[i][0] is data[i]:
+                blob = self._index_of[i][1]
+            _decompress_portion(data[i], self._np_array, self._chunkit, i, self._device_of(i), blob)
 
         with ThreadPool(processes=max(1, min(nthreads, len(data) or 1))) as pool:
             pool.map(one, range(len(data)))

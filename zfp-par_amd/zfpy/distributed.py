@@ -45,10 +45,17 @@ def _blob(s):
     return bytes(b) if b else b""
 
 
+def _peer(dist, group, r):
+    """Global rank of rank r of `group` (point-to-point ops address global ranks)."""
+    return r if group is None else dist.get_global_rank(group, r)
+
+
 def gather_streams(local, nchunks, dst=0, group=None):
-    """Gather {chunk id: stream} from every rank to `dst`; returns the list of all
-    chunk streams (ZfpBytes) in chunk order on `dst`, None elsewhere.  A stream is
-    host bytes, or a uint8 device tensor on the nccl path (gathered in HBM).
+    """Gather {chunk id: stream} from every rank to `dst` (a rank of `group`);
+    returns the list of all chunk streams in chunk order on `dst`, None
+    elsewhere: plain bytes, or a ZfpBytes for a chunk that carries a block index.
+    A local stream is host bytes, or a uint8 device tensor on the nccl path
+    (gathered in HBM).
 
     Each chunk's GPU block index (variable-rate streams) travels with it, so the
     root decodes gathered chunks without scanning them.  One all-reduce carries
@@ -85,9 +92,10 @@ def gather_streams(local, nchunks, dst=0, group=None):
     ops = []
     if rank == dst:
         recv = [send if r == rank else torch.empty(per_rank[r], dtype=torch.uint8, device=dev) for r in range(world)]
-        ops = [dist.P2POp(dist.irecv, recv[r], r, group) for r in range(world) if r != rank and per_rank[r]]
+        ops = [dist.P2POp(dist.irecv, recv[r], _peer(dist, group, r), group)
+               for r in range(world) if r != rank and per_rank[r]]
     elif per_rank[rank]:
-        ops = [dist.P2POp(dist.isend, send, dst, group)]
+        ops = [dist.P2POp(dist.isend, send, _peer(dist, group, dst), group)]
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
@@ -102,16 +110,17 @@ def gather_streams(local, nchunks, dst=0, group=None):
             torch.from_numpy(host).copy_(recv[r])
         view = memoryview(host)
         ids = rank_chunks(nchunks, world, r)
+        boff = sum(int(sz[i]) for i in ids)  # the index blobs follow the streams
         off = 0
         for i in ids:
-            n = int(sz[i])
-            out[i] = ZfpBytes(view[off:off + n])
+            n, nb = int(sz[i]), int(sz[nchunks + i])
+            if nb:
+                out[i] = ZfpBytes(view[off:off + n])
+                out[i].block_index = bytes(view[boff:boff + nb])
+            else:  # no index (fixed rate): plain bytes, copied outside the GIL
+                out[i] = zfpy_c._bytes_from(host.ctypes.data + off, n)
             off += n
-        for i in ids:
-            n = int(sz[nchunks + i])
-            if n:
-                out[i].block_index = bytes(view[off:off + n])
-            off += n
+            boff += nb
     return out
 
 
@@ -153,7 +162,8 @@ def compress_chunk_to_device(zp, ichunk, tolerance=-1, rate=-1, precision=-1, de
 def compress_distributed(zp, tolerance=-1, rate=-1, precision=-1, dst=0, group=None):
     """zfp_parallel.compress across ranks: this rank compresses its chunks of the
     shared array `zp` on its current GPU, then the streams are gathered on `dst`
-    (stored in zp._compress_data there, as the single-process compress does)."""
+    (a rank of `group`; stored in zp._compress_data there, as the single-process
+    compress does)."""
     import torch
     import torch.distributed as dist
     world = dist.get_world_size(group)

@@ -151,42 +151,62 @@ class ZfpBytes(bytes):
     block_index = None
 
 
-# Stream buffers as numpy arrays.  Output: a per-thread scratch buffer reused
-# across calls (fresh pages of a new buffer cost a page fault each while the
-# device-to-host copy fills them; the header and stream writers store whole
-# words, so its old contents never reach the result), copied once into the
-# returned bytes object.  Input: np.zeros takes calloc'd pages (zeroed by the
-# kernel, outside the GIL) where ctypes.create_string_buffer memsets under it.
-# zfp_parallel's worker threads otherwise serialise on these copies.
+# Stream buffers.  Output: a per-thread scratch buffer reused across calls
+# (fresh pages of a new buffer cost a page fault each while the device-to-host
+# copy fills them; the header and stream writers store whole words, so its old
+# contents never reach the result), kept only up to _KEEP_OUT_MAX bytes so one
+# huge call does not pin its buffer for the thread's lifetime.  The result is a
+# new bytes object filled by ctypes.memmove, which runs with the GIL released:
+# zfp_parallel's worker threads copy their chunk streams concurrently instead
+# of queueing on the GIL (bytes(memoryview) copies under it).
 _tls = threading.local()
+_KEEP_OUT_MAX = 256 << 20
+
+_bytes_uninit = ctypes.pythonapi.PyBytes_FromStringAndSize
+_bytes_uninit.restype = ctypes.py_object
+_bytes_uninit.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
 
 
 def _out_buffer(size):
     a = getattr(_tls, "out", None)
-    if a is None or a.size < size:
-        a = np.empty(max(size, 1 << 20), dtype=np.uint8)
+    if a is not None and a.size >= size:
+        return a, a.ctypes.data
+    a = np.empty(max(size, 1 << 20), dtype=np.uint8)
+    if a.size <= _KEEP_OUT_MAX:
         _tls.out = a
     return a, a.ctypes.data
 
 
-def _stream_bytes(a, n, index=None):
-    """The returned stream.  A stream with a block index (variable rate) is a
-    ZfpBytes carrying it; building that bytes subclass from a buffer copies the
-    data twice under the GIL (a plain bytes object, then the subclass object).
-    A fixed-rate stream has no index and is returned as plain bytes -- one
-    copy, as the reference's zfpy returns -- which halves the host time of
-    zfp_parallel's fixed-rate chunks (about 29 ms per 64 MB stream before)."""
+def _bytes_from(addr, n):
+    """A new bytes object holding n bytes from address addr, copied outside the GIL."""
+    out = _bytes_uninit(None, n)  # uninitialised storage, refcount 1, hash not yet cached
+    ctypes.memmove(ctypes.cast(ctypes.c_char_p(out), ctypes.c_void_p).value, addr, n)
+    return out
+
+
+def _stream_bytes(obuf, n, index=None):
+    """The returned stream.  A fixed-rate stream (no block index) is plain bytes,
+    as the reference's zfpy returns, made by one copy with the GIL released.  A
+    variable-rate stream with a block index is a ZfpBytes carrying it; building
+    that bytes subclass from a buffer copies the data twice under the GIL (a
+    plain bytes object, then the subclass object), so zfp_parallel keeps its
+    chunks' indexes beside plain bytes instead (_compress_portion)."""
     if index is None:
-        return bytes(memoryview(a)[:n])
-    out = ZfpBytes(memoryview(a)[:n])
+        return _bytes_from(obuf.ctypes.data, n)
+    out = ZfpBytes(memoryview(obuf)[:n])
     out.block_index = index
     return out
 
 
 def _in_buffer(compressed_data):
-    """The stream plus one spare zero word (the reader peeks a word past the end)."""
+    """(array, address) of the stream for the C reader.  A stream of whole 64-bit
+    words -- every stream zfp writes is flushed to a word -- is read in place
+    (the library copies whole words only, and never writes to it); otherwise it
+    is copied into a zeroed buffer padded to a whole word plus one spare word."""
     src = np.frombuffer(compressed_data, dtype=np.uint8)
-    a = np.zeros(src.size + 8, dtype=np.uint8)
+    if src.size and src.size % 8 == 0:
+        return src, src.ctypes.data
+    a = np.zeros((src.size + 15) // 8 * 8, dtype=np.uint8)
     a[:src.size] = src
     return a, a.ctypes.data
 
@@ -280,7 +300,7 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
             _lib.zfp_stream_set_hip_device(stream, device)
         _set_compression_mode(stream, type_none, ndim, tolerance, rate, precision)
         maxsize = _lib.zfp_stream_maximum_size(stream, field)
-        arr, buf = _out_buffer(maxsize)
+        obuf, buf = _out_buffer(maxsize)
         bstream = _lib.stream_open(buf, maxsize)
         _lib.zfp_stream_set_bit_stream(stream, bstream)
         _lib.zfp_stream_rewind(stream)
@@ -289,7 +309,7 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
         n = _lib.zfp_compress(stream, field)
         if n == 0:
             raise RuntimeError("Failed to write to stream")
-        return _stream_bytes(arr, n, _export_index(stream))
+        return _stream_bytes(obuf, n, _export_index(stream))
     finally:
         _lib.zfp_field_free(field)
         _lib.zfp_stream_close(stream)
@@ -316,10 +336,9 @@ def decompress_numpy(compressed_data, *, device=-1):
     """Decompress a stream written with a full header (pyx:533-557)."""
     if compressed_data is None:
         raise TypeError("compressed_data cannot be None")
-    arr, buf = _in_buffer(compressed_data)
-    data = memoryview(arr)[:-8]
+    ibuf, buf = _in_buffer(compressed_data)
     field = _lib.zfp_field_alloc()
-    bstream = _lib.stream_open(buf, len(data))
+    bstream = _lib.stream_open(buf, ibuf.size)
     stream = _lib.zfp_stream_open(bstream)
     try:
         if device >= 0:
@@ -346,9 +365,8 @@ def _decompress(compressed_data, ztype, shape, out=None, tolerance=-1, rate=-1, 
         raise ValueError("User-provided shape has too many dimensions (up to 4 supported)")
     if len(shape) <= 0:
         raise ValueError("User-provided shape needs at least one dimension")
-    arr, buf = _in_buffer(compressed_data)
-    data = memoryview(arr)[:-8]
-    bstream = _lib.stream_open(buf, len(data))
+    ibuf, buf = _in_buffer(compressed_data)
+    bstream = _lib.stream_open(buf, ibuf.size)
     stream = _lib.zfp_stream_open(bstream)
     dtype = ztype_to_dtype(ztype)
     zshape = [int(x) for x in itertools.islice(itertools.chain(reversed(shape), itertools.repeat(0)), 4)]
@@ -384,10 +402,9 @@ def header(compressed_data):
     """Stream header as a dict (pyx:596-650; `expert.maxbits` reports minbits as the reference does)."""
     if compressed_data is None:
         raise TypeError("compressed_data cannot be None")
-    arr, buf = _in_buffer(compressed_data)
-    data = memoryview(arr)[:-8]
+    ibuf, buf = _in_buffer(compressed_data)
     field = _lib.zfp_field_alloc()
-    bstream = _lib.stream_open(buf, len(data))
+    bstream = _lib.stream_open(buf, ibuf.size)
     stream = _lib.zfp_stream_open(bstream)
     try:
         if _lib.zfp_read_header(stream, field, HEADER_FULL) == 0:
@@ -491,10 +508,10 @@ def _init_field_raw(py_raw_array, chunkit):
     return _make_field(_raw_pointer(py_raw_array), dtype_to_ztype(chunkit.dtype), shape, strides)
 
 
-def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1, precision=-1, write_header=True,
-                           *, device=-1):
-    """Compress one chunk into a self-contained stream: full whole-field header + the chunk's blocks
-    (pyx:330-376).  The buffer reserves header room (the reference under-allocates, SURVEY A.1)."""
+def _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision, write_header, device, plain):
+    """compress_numpy_portion's work.  plain=False: its return value (a ZfpBytes
+    when the stream has a block index); plain=True: (plain bytes, index blob or
+    None), one GIL-free copy whatever the mode (zfp_parallel keeps the blobs)."""
     if py_raw_array is None:
         raise TypeError("Input array cannot be None")
     _one_mode(tolerance, rate, precision)
@@ -507,7 +524,7 @@ def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1,
         _set_compression_mode(stream, type_none, chunkit.ndim, tolerance, rate, precision)
         ck = chunkit.chunk_ptr(ichunk)
         maxsize = _lib.zfp_stream_maximum_size_chunk(stream, field, ck) + (HEADER_MAX_BITS + 63) // 64 * 8 + 8
-        arr, buf = _out_buffer(maxsize)
+        obuf, buf = _out_buffer(maxsize)
         bstream = _lib.stream_open(buf, maxsize)
         _lib.zfp_stream_set_bit_stream(stream, bstream)
         _lib.zfp_stream_rewind(stream)
@@ -516,7 +533,10 @@ def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1,
         n = _lib.zfp_compress_chunk(stream, ck, field)
         if n == 0:
             raise RuntimeError("Failed to write to stream")
-        return _stream_bytes(arr, n, _export_index(stream))
+        blob = _export_index(stream)
+        if plain:
+            return _bytes_from(buf, n), blob
+        return _stream_bytes(obuf, n, blob)
     finally:
         _lib.zfp_field_free(field)
         _lib.zfp_stream_close(stream)
@@ -524,15 +544,26 @@ def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1,
             _lib.stream_close(bstream)
 
 
+def compress_numpy_portion(py_raw_array, chunkit, ichunk, tolerance=-1, rate=-1, precision=-1, write_header=True,
+                           *, device=-1):
+    """Compress one chunk into a self-contained stream: full whole-field header + the chunk's blocks
+    (pyx:330-376).  The buffer reserves header room (the reference under-allocates, SURVEY A.1)."""
+    return _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision, write_header, device, False)
+
+
 def decompress_numpy_portion(compressed_data, py_raw_array, chunkit, ichunk, *, device=-1):
     """Decompress one chunk stream into its box of the shared array (pyx:559-593).  Like the
     reference, zfp_read_header resets the field strides to contiguous and nothing is returned."""
+    _decompress_portion(compressed_data, py_raw_array, chunkit, ichunk, device,
+                        getattr(compressed_data, "block_index", None))
+
+
+def _decompress_portion(compressed_data, py_raw_array, chunkit, ichunk, device, blob):
     if compressed_data is None:
         raise TypeError("compressed_data cannot be None")
     field = _init_field_raw(py_raw_array, chunkit)
-    arr, buf = _in_buffer(compressed_data)
-    data = memoryview(arr)[:-8]
-    bstream = _lib.stream_open(buf, len(data))
+    ibuf, buf = _in_buffer(compressed_data)
+    bstream = _lib.stream_open(buf, ibuf.size)
     stream = _lib.zfp_stream_open(bstream)
     idx = None
     try:
@@ -540,7 +571,7 @@ def decompress_numpy_portion(compressed_data, py_raw_array, chunkit, ichunk, *, 
             _lib.zfp_stream_set_hip_device(stream, device)
         if _lib.zfp_read_header(stream, field, HEADER_FULL) == 0:
             raise ValueError("Failed to read required zfp header")
-        idx = _attach_index(stream, getattr(compressed_data, "block_index", None))
+        idx = _attach_index(stream, blob)
         ret = _lib.zfp_decompress_chunk(stream, chunkit.chunk_ptr(ichunk), field)
         if ret == 0:
             raise RuntimeError("error during zfp decompression")

@@ -27,10 +27,10 @@ with its status.  --dry-run runs the launcher, barriers and max-over-ranks
 timing on CPU with gloo (a numpy copy stands in for the codec) -- for tests.
 
 Printed JSON (rank 0): the contract keys plus
-  roofline      dominant kernel (encode3_aligned) against HBM peak: achieved =
+  roofline      dominant kernel (c2: encode3_aligned_full) against HBM peak: achieved =
                 algorithmic bytes per launch (4 B read + R/8 B written per value)
                 / mean kernel time from HIP events on the kernel's own stream;
-                traffic = PMC HBM bytes per launch from profiles/*pmc*.json
+                traffic = PMC HBM bytes per launch from profiles/<round>_pmc_<workload>.json
                 (rocprofv3 pass, gfx950 FETCH_SIZE x2 correction) or null
   cpu_baseline  the reference itself (oracle/_ref/libzfp_ref.so, compiled from
                 /root/reference), OpenMP, every core this process may use, on
@@ -123,16 +123,19 @@ def load_capi(path):
     return ZfpCAPI(path)
 
 
-def traffic_from_profiles(kernel="encode3_aligned"):
-    """Per-launch HBM bytes of the dominant kernel from a committed PMC summary, if any."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc*.json")))
+def traffic_from_profiles(workload, kernel_prefix):
+    """Per-launch HBM bytes of the workload's dominant kernel from the newest committed
+    PMC summary profiles/<round>_pmc_<workload>.json (tools/pmc_summary.py output: a
+    rocprofv3 --pmc pass of this bench command, FETCH_SIZE x2 + WRITE_SIZE), if any."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_%s.json" % workload)))
     for f in reversed(files):
         try:
             d = json.load(open(f))
-            if kernel in d and d[kernel].get("hbm_bytes_per_launch"):
-                return d[kernel]["hbm_bytes_per_launch"], os.path.basename(f)
         except Exception:
             continue
+        for k, v in d.items():
+            if k.startswith(kernel_prefix) and isinstance(v, dict) and v.get("hbm_bytes_per_launch"):
+                return v["hbm_bytes_per_launch"], os.path.basename(f)
     return None, None
 
 
@@ -189,15 +192,16 @@ def cpu_baseline(field_np, mode, param, threads):
 
 # per workload: BASELINE config, dims, scalar, mode, dominant kernel, CPU-baseline sample (leading slab)
 WORKLOADS = {
-    "c2": dict(metric=METRIC, cfg="configs[1]", dtype="f32", mode="rate", param=16, kernel="encode3_aligned<float>",
-               sample_planes=None),
+    "c2": dict(metric=METRIC, cfg="configs[1]", dtype="f32", mode="rate", param=16,
+               kernel="encode3_aligned_full<float>", sample_planes=None, pmc="encode3_aligned_full<float"),
     "c3": dict(metric="GB/s uncompressed, 3D float64 fixed-precision-32 encode, device-resident", cfg="configs[2]",
                dtype="f64", mode="precision", param=32, kernel="encode3_general<double, hi planes>",
-               sample_planes=256),
+               sample_planes=256, pmc="encode3_general<double"),
     "c4": dict(metric=METRIC, cfg="configs[3]", dtype="f32", mode="rate", param=8, kernel="encode3_aligned<float>",
-               sample_planes=None),
+               sample_planes=None, pmc="encode3_aligned<float"),
     "c5": dict(metric="GB/s uncompressed, 4D float32 reversible (lossless) encode, device-resident", cfg="configs[4]",
-               dtype="f32", mode="reversible", param=None, kernel="encode4<float, reversible>", sample_planes=4),
+               dtype="f32", mode="reversible", param=None, kernel="encode4<float, reversible>", sample_planes=4,
+               pmc="encode4<float"),
 }
 
 
@@ -341,26 +345,35 @@ def main():
         roundtrip["decode_max_abs_err"] = float((back_t - field_t).abs().max().item())
     del back_t
 
-    # gather of the chunk streams to rank 0 over RCCL (timed separately)
+    # gather of the chunk streams to rank 0 over RCCL (timed separately): every rank
+    # sends exactly its stream (point to point, no padding to the largest), as
+    # zfpy.distributed.gather_streams does
     gather = None
     if distributed:
-        sizes = torch.tensor([nbytes], device=dev, dtype=torch.int64)
-        all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
-        dist.all_gather(all_sizes, sizes)
-        mx = int(max(s.item() for s in all_sizes))
-        send = out_t[:mx]
-        recv = [torch.empty(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+        sizes = torch.zeros(world, device=dev, dtype=torch.int64)
+        sizes[rank] = nbytes
+        dist.all_reduce(sizes, op=dist.ReduceOp.SUM)
+        sz = [int(x) for x in sizes.cpu().tolist()]
+        recv = [torch.empty(sz[r], dtype=torch.uint8, device=dev) for r in range(world)] if rank == 0 else None
         torch.cuda.synchronize()
         dist.barrier()
         g0 = time.perf_counter()
-        dist.gather(send, gather_list=recv, dst=0)
+        if rank == 0:
+            ops = [dist.P2POp(dist.irecv, recv[r], r) for r in range(1, world) if sz[r]]
+            recv[0].copy_(out_t[:sz[0]])
+        else:
+            ops = [dist.P2POp(dist.isend, out_t[:sz[rank]], 0)] if sz[rank] else []
+        if ops:
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
         torch.cuda.synchronize()
         gms = (time.perf_counter() - g0) * 1e3
         gt = torch.tensor([gms], device=dev)
         dist.all_reduce(gt, op=dist.ReduceOp.MAX)
-        total_bytes = sum(int(s.item()) for s in all_sizes)
+        total_bytes = sum(sz)
         gather = {"ms": round(float(gt.item()), 3), "bytes": total_bytes,
-                  "GBps": round(total_bytes / (float(gt.item()) * 1e6), 2), "collective": "RCCL gather to rank 0"}
+                  "GBps": round(total_bytes / (float(gt.item()) * 1e6), 2),
+                  "collective": "RCCL point-to-point gather of exact-size chunk streams to rank 0"}
         del recv
 
     if rank == 0:
@@ -369,7 +382,7 @@ def main():
         stream_bytes = nvals * wl["param"] // 8 if wl["mode"] == "rate" else int(nbytes)
         alg_bytes = nvals * es + stream_bytes
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic, tsrc = traffic_from_profiles() if args.workload == "c2" else (None, None)
+        traffic, tsrc = traffic_from_profiles(args.workload, wl["pmc"])
         value = world * nvals * es / (ms * 1e-3) / 1e9
         result = {
             "metric": wl["metric"], "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,

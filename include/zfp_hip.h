@@ -123,6 +123,12 @@ int zfp_hip_last_timing(double* kernel_ms, double* total_ms);
  * the number of segment passes.  Returns 0 if that call did not scan. */
 int zfp_hip_last_scan(double* scan_ms, int* passes);
 
+/* 1 if the most recent zfp_hip_decompress on this thread was handed an index
+ * that passed the stream fingerprint but whose block lengths disagreed with
+ * the decoded blocks (an index made for another stream): that call decoded
+ * the stream again after an index scan, so its output is still correct. */
+int zfp_hip_last_stale_index(void);
+
 /*
  * Device scratch: calls borrow a context (HIP stream + reusable buffers) from
  * a process-wide pool, so scratch is bounded by the peak number of concurrent

@@ -165,7 +165,8 @@ class ZfpCAPI:
                                 ("zfp_hip_index_free", None, [vp]), ("zfp_hip_device_count", i32, []),
                                 ("zfp_hip_last_timing", i32, [vp, vp]), ("zfp_hip_last_error", ctypes.c_char_p, []),
                                 ("zfp_hip_last_scan", i32, [vp, vp]), ("zfp_hip_scratch_bytes", sz, []),
-                                ("zfp_hip_release_scratch", i32, [])]:
+                                ("zfp_hip_release_scratch", i32, []), ("zfp_hip_last_stale_index", i32, []),
+                                ("zfp_hip_index_export", sz, [vp, vp, sz]), ("zfp_hip_index_import", vp, [vp, sz])]:
             fn = getattr(self.lib, name)
             fn.restype = res
             fn.argtypes = args

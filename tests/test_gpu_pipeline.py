@@ -73,7 +73,7 @@ def test_pipelined_stream_and_roundtrip_match_oracle(product, oracle, slabs, sha
         if product.last_index:
             product.lib.zfp_hip_index_free(product.last_index)
             product.last_index = None
-        product.keep_index = False
+        product.keep_index = True  # the fixture's setting (enable_index)
 
 
 @pytest.mark.parametrize("mode,param", [("rate", 8), ("rate", 12), ("precision", 20), ("reversible", None)])

@@ -232,3 +232,48 @@ def test_scan_4d_at_scale_matches_index_and_oracle(product, oracle, n, dtype, mo
         assert no_idx.tobytes() == arr.tobytes()
     print("%d^4 %s %s: %d B stream, scan %.3f ms in %d passes" % (n, np.dtype(dtype).name, mode, len(data),
                                                                  scan[0], scan[1]))
+
+
+@pytest.mark.parametrize("shape,dtype,mode,param,params", [
+    ((40, 44, 48), np.float64, "precision", 32, params_precision(32)),
+    ((12, 16, 16, 20), np.float32, "reversible", None, params_reversible()),
+])
+def test_stale_index_with_matching_fingerprint_is_detected(product, oracle, shape, dtype, mode, param, params):
+    """an index whose fingerprint (stream words sampled, total bits)
+    matches but whose block lengths do not -- here two adjacent blocks of one
+    wave, one 3 bits longer and the next 3 bits shorter, so every wave start and
+    the total are unchanged -- must not decode wrong data.  The decode kernels
+    compare every block's decoded length with its index entry; a difference
+    makes the call decode again after a scan (zfp_hip_last_stale_index)."""
+    import ctypes
+    rng = np.random.default_rng(21)
+    arr = _field(shape, dtype, rng, "smooth")
+    data = product.compress(arr, mode, param)
+    idx = product.last_index
+    lib = product.lib
+    n = lib.zfp_hip_index_export(idx, None, 0)
+    blob = ctypes.create_string_buffer(n)
+    assert lib.zfp_hip_index_export(idx, blob, n) == n
+    lib.zfp_hip_index_free(idx)
+    product.last_index = None
+    want, _ = _oracle_decode(oracle, data, shape, dtype, params)
+    # the exported index as is: decoded with it, no scan, not stale
+    good = lib.zfp_hip_index_import(blob, n)
+    got, _ = product.decompress(data, shape, dtype, mode, param, index=good)
+    assert got.tobytes() == want.tobytes()
+    assert product.last_scan() is None and lib.zfp_hip_last_stale_index() == 0
+    lib.zfp_hip_index_free(good)
+    # two adjacent lengths changed by +-3 (header: 10 words, then uint16 lengths)
+    raw = bytearray(blob.raw)
+    lens = np.frombuffer(raw, dtype=np.uint16, count=int(np.frombuffer(raw, np.uint64, 2)[1]), offset=80).copy()
+    lens[5] += 3
+    lens[6] -= 3
+    raw[80:80 + lens.nbytes] = lens.tobytes()
+    bad = lib.zfp_hip_index_import(bytes(raw), n)
+    assert bad
+    got, nb = product.decompress(data, shape, dtype, mode, param, index=bad)
+    lib.zfp_hip_index_free(bad)
+    assert nb == len(data)
+    assert lib.zfp_hip_last_stale_index() == 1
+    assert product.last_scan() is not None
+    assert got.tobytes() == want.tobytes()

@@ -142,13 +142,18 @@ def test_hot_kernels_use_no_scratch():
     """The float kernels (C2/C4/C5 paths) and the f64 decoders without short
     slots keep their plane registers in VGPRs: no private (scratch) segment.
     Scratch here means an unrolled plane loop fell back to memory (it did once:
-    LLVM's pragma-unroll threshold), which costs HBM traffic on every launch."""
+    LLVM's pragma-unroll threshold), which costs HBM traffic on every launch.
+    Exception: the float decode4 is compiled for 4 waves per SIMD (128 VGPRs,
+    kernels4.h kDec4Waves) and spills a few scalars (<= 64 bytes per lane, no
+    plane registers), measured 20 % faster than 3 waves without spills."""
     sc = _kernel_scratch(open(LIB, "rb").read())
     assert len(sc) > 20
     hot = {k: v for k, v in sc.items()
-           if re.match(r"_ZN7zfp_amd(15encode3_(aligned|general)|7decode3|7encode4|7decode4)If", k)}
+           if re.match(r"_ZN7zfp_amd(15encode3_(aligned|general)|20encode3_aligned_full|7decode3|7encode4|7decode4)If", k)}
     assert len(hot) >= 8, sorted(sc)[:10]
-    assert all(v == 0 for v in hot.values()), {k: v for k, v in hot.items() if v}
+    bounded = {k: v for k, v in hot.items() if k.startswith("_ZN7zfp_amd7decode4If")}
+    assert bounded and all(v <= 64 for v in bounded.values()), bounded
+    assert all(v == 0 for k, v in hot.items() if k not in bounded), {k: v for k, v in hot.items() if v and k not in bounded}
     # f64 decoders without short slots: P[32] must stay in registers
     dnon = {k: v for k, v in sc.items() if k.startswith("_ZN7zfp_amd7decode3Id") and k.endswith("Lb0EEEvPT_NS_8GeometryENS_11CodecParamsENS_10DecodeArgsE")}
     assert dnon and all(v == 0 for v in dnon.values()), dnon

@@ -10,6 +10,7 @@
 #include <vector>
 #include <string>
 #include "kernels3.h"
+#include "ilv.h"
 using namespace zfp_amd;
 
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
@@ -103,6 +104,7 @@ template <int G, bool SYNC = true, bool WAIT0 = true>
 __global__ __launch_bounds__(256, 3) void enc_gate(const float* __restrict__ data, Geometry g, CodecParams cp,
                                                  uint64_t* __restrict__ out, uint32_t sw, uint32_t sdw, uint32_t magic_c)
 {
+  constexpr int MORPH = 0;
   __shared__ uint32_t lut[512];
   __shared__ uint32_t gate;
   extern __shared__ uint32_t ldsw[];
@@ -138,10 +140,29 @@ __global__ __launch_bounds__(256, 3) void enc_gate(const float* __restrict__ dat
     __builtin_amdgcn_s_waitcnt(0xc07f);
   }
   __builtin_amdgcn_wave_barrier();
-  OrSlot os{reinterpret_cast<uint64_t*>(wslot + (size_t)lane * sdw), sdw - 1};
-  encode_block3<float, false, true>(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+  if (!(MORPH & 4) || b < g.nblocks) {
+    OrSlot os{reinterpret_cast<uint64_t*>(wslot + (size_t)lane * sdw), sdw - 1};
+    encode_block3<float, false, true>(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+  }
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+  if (MORPH & 1) {
+    if (first >= g.nblocks)
+      return;
+    const uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
+    const uint32_t hw = sw >> 1, chunks = (uint32_t)nb * hw;
+    uint64_t* dst = out + first * sw;
+    if ((sw & 1) == 0) {
+      for (uint32_t c = lane; c < chunks; c += 64) {
+        const uint32_t l = div_magic(c, magic_c);
+        const uint32_t* s = wslot + (size_t)l * sdw + 4 * (c - l * hw);
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u4{s[0], s[1], s[2], s[3]}, reinterpret_cast<u4*>(dst + 2 * c));
+      }
+    }
+    if (!(MORPH & 2)) __builtin_amdgcn_s_waitcnt(0x0f70);
+    return;
+  }
   const uint32_t hw = sw >> 1, chunks = 64 * hw;
   uint64_t* dst = out + first * sw;
   for (uint32_t c = lane; c < chunks; c += 64) {
@@ -149,6 +170,143 @@ __global__ __launch_bounds__(256, 3) void enc_gate(const float* __restrict__ dat
     const uint32_t* s = wslot + (size_t)l * sdw + 4 * (c - l * hw);
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     __builtin_nontemporal_store(u4{s[0], s[1], s[2], s[3]}, reinterpret_cast<u4*>(dst + 2 * c));
+  }
+}
+
+// round 4: the product kernel plus an L2/MALL prefetch of the field rows of
+// the workgroup DIST launches later (on the same XCD when DIST % 8 == 0):
+// LDS-DMA loads into a 1 KB dummy area (no VGPRs held), so that workgroup's
+// own loads hit on-die caches.
+template <uint32_t DIST, int PRIO, int WPG = 4, bool GUARD = false, int MORPH = 0>
+__global__ __launch_bounds__(64 * WPG, 3) void enc_pf(const float* __restrict__ data, Geometry g, CodecParams cp,
+                                               uint64_t* __restrict__ out, uint32_t sw, uint32_t sdw, uint32_t magic_c)
+{
+  __shared__ uint32_t lut[512];
+  __shared__ uint32_t dummy[256];
+  extern __shared__ uint32_t ldsw[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint32_t* wslot = ldsw + (size_t)wv * 64 * sdw;
+  const uint64_t w = (uint64_t)blockIdx.x * WPG + wv;
+  const uint64_t first = w * 64;
+  const uint64_t b = first + lane;
+  float v[64];
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  BlockPos p{};
+  if (!GUARD || b < g.nblocks) {
+    p = block_pos(g, b, 3);
+    gather3<float, true>(v, data, g, p);
+  }
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&kCoderTables);
+    uint4* dst = reinterpret_cast<uint4*>(lut);
+    dst[lane] = src[lane];
+    dst[lane + 64] = src[lane + 64];
+  }
+  const uint64_t bp = b + (uint64_t)DIST * 256;
+  if (DIST && first + (uint64_t)DIST * 256 < g.nblocks) {
+    const BlockPos pp = block_pos(g, bp, 3);
+    const float* o = data + pp.off;
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int j = 0; j < 4; j++)
+        __builtin_amdgcn_global_load_lds((const void*)(o + j * g.s[1] + k * g.s[2]),
+                                         (__attribute__((address_space(3))) void*)dummy, 16, 0, 0);
+  }
+  {
+    uint4* z = reinterpret_cast<uint4*>(wslot);
+    for (uint32_t i = lane; i < 16 * sdw; i += 64)
+      z[i] = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!(MORPH & 4) || b < g.nblocks) {
+    OrSlot os{reinterpret_cast<uint64_t*>(wslot + (size_t)lane * sdw), sdw - 1};
+    encode_block3<float, false, true>(os, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+  }
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  if (MORPH & 1) {
+    if (first >= g.nblocks)
+      return;
+    const uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
+    const uint32_t hw = sw >> 1, chunks = (uint32_t)nb * hw;
+    uint64_t* dst = out + first * sw;
+    if ((sw & 1) == 0) {
+      for (uint32_t c = lane; c < chunks; c += 64) {
+        const uint32_t l = div_magic(c, magic_c);
+        const uint32_t* s = wslot + (size_t)l * sdw + 4 * (c - l * hw);
+        typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(u4{s[0], s[1], s[2], s[3]}, reinterpret_cast<u4*>(dst + 2 * c));
+      }
+    }
+    if (!(MORPH & 2)) __builtin_amdgcn_s_waitcnt(0x0f70);
+    return;
+  }
+  const uint32_t hw = sw >> 1, chunks = 64 * hw;
+  uint64_t* dst = out + first * sw;
+  for (uint32_t c = lane; c < chunks; c += 64) {
+    const uint32_t l = div_magic(c, magic_c);
+    const uint32_t* s = wslot + (size_t)l * sdw + 4 * (c - l * hw);
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(u4{s[0], s[1], s[2], s[3]}, reinterpret_cast<u4*>(dst + 2 * c));
+  }
+  if (!(MORPH & 2)) __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the prefetch has landed before the workgroup's LDS is released
+}
+
+// round 4: interleaved (conflict-free) LDS slots, each lane stores its own
+// block with 16-byte strided stores (ilv.h)
+template <int PRIO, int OWN>
+__global__ __launch_bounds__(256, 3) void enc_ilv(const float* __restrict__ data, Geometry g, CodecParams cp,
+                                                uint64_t* __restrict__ out, uint32_t rows)
+{
+  __shared__ uint32_t lut[512];
+  extern __shared__ uint32_t ldsw[];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  uint32_t* wreg = ldsw + (size_t)wv * 64 * rows;
+  const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
+  const uint64_t first = w * 64;
+  const uint64_t b = first + lane;
+  float v[64];
+  if (PRIO) __builtin_amdgcn_s_setprio(PRIO);
+  BlockPos p = block_pos(g, b, 3);
+  gather3<float, true>(v, data, g, p);
+  if (PRIO) __builtin_amdgcn_s_setprio(0);
+  {
+    const uint4* src = reinterpret_cast<const uint4*>(&kCoderTables);
+    uint4* dst = reinterpret_cast<uint4*>(lut);
+    dst[lane] = src[lane];
+    dst[lane + 64] = src[lane + 64];
+    uint4* z = reinterpret_cast<uint4*>(wreg);
+    for (uint32_t i = lane; i < 16 * rows; i += 64)
+      z[i] = make_uint4(0, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+  }
+  const uint32_t lanebase = lds_off(wreg) + 4u * lane;
+  ilv::encode_block_fixed_f32(lanebase, rows - 1, lut, v, cp, [&](float (&r)[64]) { gather3<float, true>(r, data, g, p); });
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+  if (OWN) {
+    u4* dst = reinterpret_cast<u4*>(out + b * 16);
+#pragma unroll
+    for (int c = 0; c < 8; c++) {
+      const uint32_t* s = wreg + lane + 256 * c;
+      __builtin_nontemporal_store(u4{s[0], s[64], s[128], s[192]}, dst + c);
+    }
+  } else {
+    // coalesced: chunk t of the wave's run = dwords 4(t%8) .. of block t/8
+    u4* dst = reinterpret_cast<u4*>(out + first * 16);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint32_t t = lane + 64 * i, l = t >> 3, c = t & 7;
+      const uint32_t* s = wreg + l + 256 * c;
+      __builtin_nontemporal_store(u4{s[0], s[64], s[128], s[192]}, dst + t);
+    }
   }
 }
 
@@ -207,7 +365,7 @@ int main(int argc, char** argv)
   unsigned long long h = 0;
   CK(hipMemcpy(&h, cs, 8, hipMemcpyDeviceToHost));
   printf("%-10s checksum %016llx\n", tag, h);
-  for (int r = 0; r < 2; r++) {
+  for (int r = 0; r < 0; r++) {
     float t;
     t = time_it([&] { hipLaunchKernelGGL(enc_gate<1>, grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
     printf("%-10s gate1     %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
@@ -233,6 +391,55 @@ int main(int argc, char** argv)
     t = time_it([&] { hipLaunchKernelGGL((encode3_aligned<float, true, false, 8>), dim3((unsigned)(g.nblocks / 512)), dim3(512),
                                          8 * 64 * sdw * 4, 0, d, g, cp, o, sw, sdw, magic_w, magic_c, 0u, (Partial*)nullptr); }, 20);
     printf("%-10s wpg8      %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+  }
+  for (int r = 0; r < 2; r++) {
+    float t;
+#define PF(D, P) \
+    t = time_it([&] { hipLaunchKernelGGL((enc_pf<D, P>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20); \
+    printf("%-10s pf%-4d p%d %.4f ms  frac %.4f\n", tag, D, P, t, gb / t * 1e3 / 8000.0);
+    PF(0, 0) PF(0, 1)
+#define MO(M) \
+    t = time_it([&] { hipLaunchKernelGGL((enc_pf<0, 0, 4, false, M>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20); \
+    printf("%-10s morph%d %.4f ms  frac %.4f\n", tag, M, t, gb / t * 1e3 / 8000.0);
+    MO(1) MO(2) MO(3) MO(4) MO(7)
+    t = time_it([&] { hipLaunchKernelGGL((enc_pf<0, 1, 4, true>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s pf0 p1 guard %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((enc_pf<0, 1, 2>), dim3((unsigned)(g.nblocks / 128)), dim3(128), 2 * 64 * sdw * 4, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s pf0 p1 wpg2 %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((enc_pf<0, 2, 2>), dim3((unsigned)(g.nblocks / 128)), dim3(128), 2 * 64 * sdw * 4, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s pf0 p2 wpg2 %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    t = time_it([&] { hipLaunchKernelGGL((enc_pf<0, 3, 4>), grid, block, lds, 0, d, g, cp, o, sw, sdw, magic_c); }, 20);
+    printf("%-10s pf0 p3      %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+  }
+  {
+    CK(hipMemset(cs, 0, 8));
+    hipLaunchKernelGGL((enc_pf<0, 1, 2>), dim3((unsigned)(g.nblocks / 128)), dim3(128), 2 * 64 * sdw * 4, 0, d, g, cp, o, sw, sdw, magic_c);
+    hipLaunchKernelGGL(checksum, dim3(1024), dim3(256), 0, 0, o, (uint64_t)(N / 4), cs);
+    unsigned long long h2 = 0;
+    CK(hipMemcpy(&h2, cs, 8, hipMemcpyDeviceToHost));
+    printf("%-10s pf checksum %016llx\n", tag, h2);
+  }
+  {
+    const uint32_t rows = slot_dwords_for(1024);  // 35
+    const size_t ilds = 4 * 64 * rows * 4;
+    for (int r = 0; r < 2; r++) {
+      float t;
+      t = time_it([&] { hipLaunchKernelGGL((enc_ilv<0, 1>), grid, block, ilds, 0, d, g, cp, o, rows); }, 20);
+      printf("%-10s ilv own p0 %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+      t = time_it([&] { hipLaunchKernelGGL((enc_ilv<1, 1>), grid, block, ilds, 0, d, g, cp, o, rows); }, 20);
+      printf("%-10s ilv own p1 %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+      t = time_it([&] { hipLaunchKernelGGL((enc_ilv<1, 0>), grid, block, ilds, 0, d, g, cp, o, rows); }, 20);
+      printf("%-10s ilv coa p1 %.4f ms  frac %.4f\n", tag, t, gb / t * 1e3 / 8000.0);
+    }
+    for (int own = 0; own < 2; own++) {
+      CK(hipMemset(cs, 0, 8));
+      if (own) hipLaunchKernelGGL((enc_ilv<1, 1>), grid, block, ilds, 0, d, g, cp, o, rows);
+      else hipLaunchKernelGGL((enc_ilv<1, 0>), grid, block, ilds, 0, d, g, cp, o, rows);
+      hipLaunchKernelGGL(checksum, dim3(1024), dim3(256), 0, 0, o, (uint64_t)(N / 4), cs);
+      unsigned long long h2 = 0;
+      CK(hipMemcpy(&h2, cs, 8, hipMemcpyDeviceToHost));
+      printf("%-10s ilv%d checksum %016llx\n", tag, own, h2);
+    }
   }
   for (int G : {1, 2}) {
     CK(hipMemset(cs, 0, 8));

@@ -28,7 +28,7 @@ for k, v in out.items():
         v["hbm_write_bytes_per_launch"] = int(v["WRITE_SIZE"] * 1024)
         v["hbm_bytes_per_launch"] = v["hbm_read_bytes_per_launch"] + v["hbm_write_bytes_per_launch"]
 for k in list(out):
-    for short in ("encode3_aligned", "decode3"):
+    for short in ("encode3_aligned_full", "encode3_aligned", "decode3"):
         if k.startswith(short + "<float"):
             out.setdefault(short, dict(out[k], kernel=k))
 json.dump(out, open(os.path.join(d, "summary.json"), "w"), indent=1)

@@ -624,10 +624,11 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
 }
 
 // Decode the quad's block (invalid quads decode nothing but take part in the
-// wave-wide exchange); lane r receives slice w = r.
+// wave-wide exchange); lane r receives slice w = r.  Returns the block's length
+// in bits including minbits padding (0 for an invalid quad), the encoder's.
 template <typename S, bool REV, bool HALF = false>
-__device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const CodecParams& cp,
-                                              typename Traits<S>::Int* X, const uint32_t* tab, bool valid)
+__device__ __forceinline__ uint32_t decode_block4(WordReader& rd, S (&v)[64], const CodecParams& cp,
+                                                  typename Traits<S>::Int* X, const uint32_t* tab, bool valid)
 {
   using T = Traits<S>;
   using Int = typename T::Int;
@@ -640,6 +641,7 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
     q[i] = 0;
   int emax = 0;
   uint32_t kind = 0;  // 0: zero block, 1: block-floating-point, 2: reinterpreted bits
+  uint32_t used = 0;
   if constexpr (std::is_integral<S>::value) {
     // integer blocks (decode.c:271-287, revdecode.c:34-52)
     if (valid) {
@@ -649,7 +651,8 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
         bits = T::kPbits;
       }
       uint64_t P[PREC];
-      decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+      used = bits + decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+      used = used < cp.minbits ? cp.minbits : used;
       pin_registers(P);
       if constexpr (PREC == 32)
         coeffs_from_planes<false>(q, P);
@@ -661,8 +664,10 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
 #pragma unroll
     for (int i = 0; i < 64; i++)
       v[i] = (S)q[i];
-    return;
+    return used;
   } else {
+    if (valid)
+      used = 1u < cp.minbits ? cp.minbits : 1u;  // a zero block: one bit and the padding
     if (valid && rd.read1()) {
       uint32_t bits = 1;
       uint32_t prec;
@@ -683,7 +688,8 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
         kind = 1;
       }
       uint64_t P[PREC];
-      decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+      used = bits + decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
+      used = used < cp.minbits ? cp.minbits : used;
       pin_registers(P);
       if constexpr (PREC == 32)
         coeffs_from_planes<false>(q, P);
@@ -708,6 +714,7 @@ __device__ __forceinline__ void decode_block4(WordReader& rd, S (&v)[64], const 
       for (int i = 0; i < 64; i++)
         v[i] = 0;
     }
+    return used;
   }
 }
 

@@ -40,6 +40,8 @@ struct OvfEntry {
 // HALF: exchange areas shared by quads q and q + 8 (block4.h exchange_fwd), so
 // the LDS region is max(16 slots, 8 exchange areas); with a.ovf the slots are
 // short (see OvfEntry).
+// (Compiled for 4 waves per SIMD the f32 reversible encoder spills and ran
+// 1.56 -> 1.92 ms on 128^4; it is left unbounded: 140 VGPRs, 3 waves.)
 template <typename S, bool VEC, bool REV, bool HALF = false>
 __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geometry g, CodecParams cp, GeneralArgs a)
 {
@@ -195,8 +197,17 @@ __global__ __launch_bounds__(64) void encode4_patch(const S* __restrict__ data, 
   }
 }
 
+// Waves per SIMD the decoder is compiled for: float blocks at 4 (<= 128 VGPRs,
+// 20-32 bytes of spills; unbounded they take 131-135, i.e. 3 waves) with the
+// packed staging sized to match (kDec4WavesPerCu): 128^4 f32 reversible
+// decode 1.37 -> 1.09 ms; double blocks spill 750+ bytes at 128, so they are
+// left unbounded.
+template <typename S>
+constexpr int kDec4Waves = (sizeof(S) == 4 && !kIntField<S>) ? 4 : 1;
+template <typename S>
+constexpr uint32_t kDec4WavesPerCu = sizeof(S) == 4 ? (kIntField<S> ? 12u : 16u) : 8u;
 template <typename S, bool VEC, bool REV, bool HALF = false>
-__global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
+__global__ __launch_bounds__(64, kDec4Waves<S>) void decode4(S* __restrict__ data, Geometry g, CodecParams cp, DecodeArgs a)
 {
   using Int = typename Traits<S>::Int;
   extern __shared__ uint64_t lds[];
@@ -205,15 +216,16 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
   uint64_t* region = lds + kDec4HeadWords;
   const uint32_t lane = threadIdx.x;
   tab[lane] = kOrderTab4.t[lane];
-  const uint64_t w = blockIdx.x;
+  const uint64_t w = a.wave_list ? a.wave_list[blockIdx.x] : blockIdx.x;
   const uint64_t first = w * kBlocks4PerWave;
   const uint32_t qd = lane >> 2, r = lane & 3u;
   const uint64_t b = first + qd;
   const bool valid = b < g.nblocks;
   uint64_t start;
   uint32_t pos;
+  uint32_t len = 0;  // the block's index length (lane r == 0 of the quad)
   if (a.var) {
-    const uint32_t len = (valid && r == 0u) ? a.idx_len[b] : 0u;
+    len = (valid && r == 0u) ? a.idx_len[b] : 0u;
     pos = wave_incl_scan(len) - len;
     start = a.idx_base[w];
   } else {
@@ -234,13 +246,19 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
     // Packed (variable rate): the wave's blocks are contiguous in the stream,
     // so its segment is staged as is, one word per lane and step, and each
     // quad reads its block at its bit offset -- no slot sized for the worst
-    // block.  A segment longer than the LDS holds (rough data) sets the error
-    // flag; the host repeats the launch with padded slots.
+    // block.  A segment longer than the LDS holds (runs of long blocks) puts
+    // the wave on the overflow list, decoded by the host's second launch with
+    // padded slots.
     const uint32_t total = __shfl(pos + (r == 0u && valid ? (uint32_t)a.idx_len[b] : 0u), 4 * (nb - 1), 64);
     const uint32_t nwords = ((uint32_t)(G & 63) + total + 63) / 64 + 1;  // + 1: the window reads past the end
     if (nwords > a.packw) {
-      if (lane == 0)
-        atomicOr(a.error, 2u);
+      if (lane == 0) {
+        const uint32_t k = atomicAdd(a.ovf_count, 1u);
+        if (k < a.ovf_cap)
+          a.wave_ovf[k] = (uint32_t)w;
+        else
+          atomicOr(a.error, 2u);
+      }
       return;  // wave-uniform: a one-wave workgroup
     }
     stage_batched(
@@ -289,7 +307,9 @@ __global__ __launch_bounds__(64) void decode4(S* __restrict__ data, Geometry g, 
   rd.pos = rpos;
   S v[64];
   Int* X = reinterpret_cast<Int*>(region) + (size_t)(HALF ? (qd & 7u) : qd) * kXStride;
-  decode_block4<S, REV, HALF>(rd, v, cp, X, tab, valid);
+  const uint32_t used = decode_block4<S, REV, HALF>(rd, v, cp, X, tab, valid);
+  if (a.idx_bad && valid && r == 0u && used != len)
+    atomicOr(a.idx_bad, 1u);
   if (!valid)
     return;
   const BlockPos p = block_pos(g, b, 4);

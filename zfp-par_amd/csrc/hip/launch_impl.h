@@ -10,7 +10,14 @@ template <typename S>
 void enc3_aligned_impl(const Launch& l, bool vec, const S* f, const Geometry& g, const CodecParams& cp, uint64_t* out,
                        uint32_t sw, uint32_t sdw, uint32_t mw, uint32_t mc, uint32_t r0, Partial* parts)
 {
-  if (vec)
+  // whole workgroups, word-aligned start, even words per block (16-byte chunks)
+  const bool full = r0 == 0 && (sw & 1) == 0 && sw >= 2 && g.nblocks % (64u * kWavesPerGroup) == 0 &&
+                    (reinterpret_cast<uintptr_t>(out) & 15) == 0 && l.block.x == 64u * kWavesPerGroup;
+  if (full && vec)
+    hipLaunchKernelGGL((encode3_aligned_full<S, true>), l.grid, l.block, l.lds, l.stream, f, g, cp, out, sw, sdw, mc);
+  else if (full)
+    hipLaunchKernelGGL((encode3_aligned_full<S, false>), l.grid, l.block, l.lds, l.stream, f, g, cp, out, sw, sdw, mc);
+  else if (vec)
     hipLaunchKernelGGL((encode3_aligned<S, true, false>), l.grid, l.block, l.lds, l.stream, f, g, cp, out, sw, sdw, mw,
                        mc, r0, parts);
   else

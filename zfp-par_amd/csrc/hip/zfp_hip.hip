@@ -150,12 +150,15 @@ struct Ctx {
   Scratch field, words, status, partials, misc, ovf, fpbuf;
   Scratch scan_bm, scan_seg, scan_tiles, scan_pos;  // index scan of a stream without index
   zfp_hip_index scan_index;                         // index built by the scan
+  Scratch chk;                                      // index verification word (DecodeArgs::idx_bad)
+  uint32_t* idx_chk = nullptr;                      // set while a caller's index is being verified
 };
 
 struct Timing {
   double kernel_ms = 0, total_ms = 0, scan_ms = 0;
   int scan_passes = 0;
   bool timed = false;
+  bool stale_index = false;  // the last decompress found its index stale and scanned (zfp_hip_last_stale_index)
 };
 static thread_local Timing t_timing;
 
@@ -174,7 +177,7 @@ static void destroy_ctx(Ctx* c)
 {
   (void)hipSetDevice(c->device);
   for (Scratch* s : {&c->field, &c->words, &c->status, &c->partials, &c->misc, &c->ovf, &c->fpbuf, &c->scan_bm,
-                     &c->scan_seg, &c->scan_tiles, &c->scan_pos})
+                     &c->scan_seg, &c->scan_tiles, &c->scan_pos, &c->chk})
     free_scratch(*s);
   index_release(&c->scan_index);
   for (auto& e : c->ev)
@@ -584,11 +587,18 @@ static uint32_t short_slot_words(const Plan& p)
   return swp < 3 ? ~0u : (uint32_t)swp;
 }
 
-// Short slots for the variable-rate 4D encoder (f32/f64 fields): the region of
-// 16 slots sized for the worst case (f32 reversible: 8,462 bits, 17.3 KB)
-// limits the CU to 7 workgroups (< 2 waves per SIMD); the registers allow 3
-// (f32 reversible, 145 VGPRs) or 4 (f32 lossy).  The exchange areas are halved
-// (HALF), the slots cut to what is left; longer blocks go to encode4_patch.
+// Short slots for the variable-rate 4D encoder (f32 fields): the region of 16
+// slots sized for the worst case (f32 reversible: 8,462 bits, 17.3 KB) limits
+// the CU to 8 one-wave workgroups (2 waves per SIMD), where the registers allow
+// 3 (f32 reversible) or 4 (f32 lossy).  Slots cut to what 12 waves per CU
+// leave (blocks that code longer go to encode4_patch) measured no faster on
+// 128^4 f32 reversible (1.56 ms either way, round 4), and on the C5 chunk
+// more than 1/16 of the blocks -- the ones that fail the reversible cast test,
+// about 8,300 bits each -- overflowed, so the overflow pool ran out and the
+// launch was repeated with full slots (46 -> 90 ms per call).  So full-size
+// slots by default; ZFP_HIP_SLOT_WORDS=n forces n-word slots (tests of the
+// overflow and patch path).  (Rounds 2-3 sized them by waves per SIMD instead
+// of per CU, which left them full-size as well.)
 template <typename S>
 static uint32_t short_slot_words4(const Plan& p)
 {
@@ -596,13 +606,7 @@ static uint32_t short_slot_words4(const Plan& p)
     return ~0u;
   if (const char* e = getenv("ZFP_HIP_SLOT_WORDS"))  // tests: force overflows
     return (uint32_t)atoi(e) | 1u;
-  const bool rev = p.cp.minexp < kMinExp;
-  const int groups = rev ? 3 : 4;
-  const int64_t region = (int64_t)(160 * 1024) / groups - (int64_t)kEnc4HeadWords * 8;
-  int64_t swp = region / (8 * kBlocks4PerWave);
-  if ((swp & 1) == 0)
-    swp--;
-  return swp < 5 ? ~0u : (uint32_t)swp;
+  return ~0u;
 }
 
 template <typename S>
@@ -778,6 +782,7 @@ static int run_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, 
   a.g0 = g0;
   a.var = p.fixed ? 0 : 1;
   a.maxbits = p.cp.maxbits;
+  a.idx_bad = p.fixed ? nullptr : c->idx_chk;
   const uint32_t per_block = p.fixed ? p.cp.maxbits : p.max_len;
   a.W = (per_block + 63) / 64 + 1;  // peek64 at the budget end reads one word past it
   a.swp = a.W | 1;
@@ -793,55 +798,76 @@ static int run_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, 
   const bool half = !kIntField<S>;
   const size_t xfull = (size_t)kBlocks4PerWave * kXStride * sizeof(Int);
   // variable rate, f32/f64: the wave's segment (its 16 blocks, contiguous in
-  // the stream) staged back to back, sized for 16 worst-case blocks so every
-  // segment fits -- about the LDS of 16 padded slots, but the staging reads
-  // only the segment's words, where padded slots read 16 worst-case blocks'
-  // worth of words for every wave (128^4 f32 reversible decode 1.90 -> 1.46 ms).
-  // ZFP_HIP_PACK_WORDS=n stages n words instead (tests: a segment past n
-  // words sets the error flag and the launch is repeated with padded slots);
-  // ZFP_HIP_FULL_SLOTS=1 padded slots only.
+  // the stream) staged back to back in what the kernel's VGPR-bound number of
+  // waves per CU leaves of the LDS (kDec4WavesPerCu); the staging reads only
+  // the segment's words, where padded slots read 16 worst-case blocks' worth
+  // for every wave.  A wave whose segment does not fit (runs of long blocks: on
+  // the C5 field 2.6 % of the waves at 16 waves per CU) goes on a list that a
+  // second launch decodes with padded slots.  ZFP_HIP_PACK_WORDS=n stages n words instead
+  // (tests: many waves take the second launch); ZFP_HIP_FULL_SLOTS=1 padded
+  // slots only.
   uint32_t packw = 0;
   if (!p.fixed && half && !getenv("ZFP_HIP_FULL_SLOTS")) {
-    packw = (uint32_t)((126ull + (uint64_t)kBlocks4PerWave * per_block) / 64 + 1);
+    const uint32_t waves_per_cu = kDec4WavesPerCu<S>;
+    const uint32_t fit = (uint32_t)(((160u * 1024u) / waves_per_cu - kDec4HeadWords * 8) / 8);
+    const uint32_t worst = (uint32_t)((126ull + (uint64_t)kBlocks4PerWave * per_block) / 64 + 1);
+    packw = std::min(fit, worst);
     if (const char* e = getenv("ZFP_HIP_PACK_WORDS"))
       packw = (uint32_t)atoi(e);
-    if ((size_t)packw * 8 < xfull / 2 || (size_t)kDec4HeadWords * 8 + (size_t)packw * 8 > 160 * 1024)
+    if ((size_t)packw * 8 < xfull / 2)
+      packw = (uint32_t)(xfull / 16);  // the exchange areas need that much anyway
+    if ((size_t)kDec4HeadWords * 8 + (size_t)packw * 8 > 160 * 1024)
       packw = 0;
   }
-  for (int attempt = 0; attempt < 2; attempt++) {
-    a.packw = attempt == 0 ? packw : 0u;
-    const size_t region = a.packw ? std::max<size_t>((size_t)a.packw * 8, xfull / 2)
-                                  : std::max<size_t>((size_t)kBlocks4PerWave * a.swp * 8, half ? xfull / 2 : xfull);
+  const bool rev = p.cp.minexp < kMinExp;
+  auto launch = [&](uint32_t pw, dim3 grid) -> int {
+    a.packw = pw;
+    const size_t region = pw ? std::max<size_t>((size_t)pw * 8, xfull / 2)
+                             : std::max<size_t>((size_t)kBlocks4PerWave * a.swp * 8, half ? xfull / 2 : xfull);
     const size_t lds = (size_t)kDec4HeadWords * 8 + region;
     if (lds > 160 * 1024)
       return fail("zfp_hip: 4D block size too large for LDS staging (%u bits)", per_block);
-    if (a.packw) {
-      if (!ensure(c->misc, 64))
-        return 0;
-      HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, c->stream));
-      a.error = (uint32_t*)((char*)c->misc.p + 12);
-    }
-    dim3 grid((unsigned)nwaves), block(64);
-    HIP_TRY(hipEventRecord(c->ev[1], c->stream));
-    const bool rev = p.cp.minexp < kMinExp;
     if constexpr (kIntField<S>)
-      launch_decode4_int(p.type, rev, p.vec, c->stream, grid, block, lds, d_field, p.g, p.cp, a);
+      launch_decode4_int(p.type, rev, p.vec, c->stream, grid, dim3(64), lds, d_field, p.g, p.cp, a);
     else
-      launch_decode4(Launch{grid, block, lds, c->stream}, p.vec, rev, d_field, p.g, p.cp, a);
+      launch_decode4(Launch{grid, dim3(64), lds, c->stream}, p.vec, rev, d_field, p.g, p.cp, a);
     HIP_TRY(hipGetLastError());
+    return 1;
+  };
+  HIP_TRY(hipEventRecord(c->ev[1], c->stream));
+  if (!packw) {
+    if (!launch(0, dim3((unsigned)nwaves)))
+      return 0;
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
-    if (!a.packw)
-      return 1;
-    uint32_t err = 0;
-    HIP_TRY(hipMemcpyAsync(&err, a.error, 4, hipMemcpyDeviceToHost, c->stream));
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    if (!(err & 2u))
-      return 1;
-    if (getenv("ZFP_HIP_VERBOSE"))
-      fprintf(stderr, "zfp_hip: decode4 segment past %u staged words, repeated with padded slots\n", a.packw);
+    return 1;
   }
-  return fail("zfp_hip: 4D decode staging failed with padded slots");
+  // misc: [12] error, [16] list count; ovf: the wave list
+  if (!ensure(c->misc, 64) || !ensure(c->ovf, nwaves * 4))
+    return 0;
+  HIP_TRY(hipMemsetAsync(c->misc.p, 0, 64, c->stream));
+  a.error = (uint32_t*)((char*)c->misc.p + 12);
+  a.ovf_count = (uint32_t*)((char*)c->misc.p + 16);
+  a.wave_ovf = (uint32_t*)c->ovf.p;
+  a.ovf_cap = (uint32_t)nwaves;
+  if (!launch(packw, dim3((unsigned)nwaves)))
+    return 0;
+  uint32_t n = 0;
+  HIP_TRY(hipMemcpyAsync(&n, a.ovf_count, 4, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (n) {
+    if (getenv("ZFP_HIP_VERBOSE"))
+      fprintf(stderr, "zfp_hip: decode4: %u of %llu wave segments past %u staged words, decoded with padded slots\n",
+              n, (unsigned long long)nwaves, packw);
+    a.wave_list = a.wave_ovf;
+    a.wave_ovf = nullptr;
+    if (!launch(0, dim3(n)))
+      return 0;
+    a.wave_list = nullptr;
+  }
+  HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+  return 1;
 }
+
 
 // Short staging slots for the variable-rate 3D decoder (the encoder's rule,
 // short_slot_words): words staged per block such that the kernel's VGPR-bound
@@ -884,6 +910,7 @@ static int launch_decode(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in
     a.g0 = g0;
     a.var = p.fixed ? 0 : 1;
     a.maxbits = p.cp.maxbits;
+    a.idx_bad = p.fixed ? nullptr : c->idx_chk;
     a.W = attempt == 0 ? std::min(W_full, W_short) : W_full;
     a.swp = a.W | 1;
     a.wmagic = (uint32_t)((0x100000000ull + a.W - 1) / a.W);
@@ -1699,34 +1726,43 @@ int zfp_hip_compress(const zfp_hip_job* job, const void* field_base, uint64_t* w
   return 1;
 }
 
-int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t* words, uint64_t capacity_words,
-                       uint64_t bit_offset, int device, const zfp_hip_index* index, uint64_t* end_bit)
+// One decompression with the given index (nullptr: the stream is scanned).
+// *stale: the decoded block lengths disagreed with a caller's index that had
+// passed index_matches -- the index belongs to another stream; the output is
+// garbage and the caller decodes again with a scan.
+static int decompress_once(Ctx* c, const Plan& p, const zfp_hip_job* job, void* field_base, const uint64_t* words,
+                           uint64_t capacity_words, uint64_t bit_offset, const zfp_hip_index* index,
+                           uint64_t* end_bit, bool* stale)
 {
-  Plan p;
-  if (!plan_job(job, field_base, p))
-    return 0;
-  if (!field_base || !words)
-    return fail("zfp_hip_decompress: null field or stream pointer");
-  if (zfp_hip_device_count() <= 0)
-    return fail("zfp_hip_decompress: no HIP device available");
-  CtxLease lease(device);
-  Ctx* c = lease.c;
-  if (!c)
-    return 0;
-  t_timing = Timing{};
   const size_t es = p.es;
   const uint64_t W0 = bit_offset >> 6;
   const uint32_t g0 = (uint32_t)(bit_offset & 63);
-  if (p.g.nblocks == 0) {
-    *end_bit = bit_offset;
-    return 1;
-  }
   const bool dev_field = is_device_ptr(field_base);
   const bool dev_stream = is_device_ptr(words);
   // a variable-rate stream without a matching index (made by another
   // process, another library, or for another stream or position) is scanned
   const bool have_index = !p.fixed && index_matches(c, index, p, words, dev_stream, capacity_words, bit_offset);
   const bool scan = !p.fixed && !have_index;
+  // a caller's index that passed the (sampled) fingerprint is verified exactly
+  // by the decode kernels: every block's decoded length against its entry
+  c->idx_chk = nullptr;
+  if (have_index) {
+    if (!ensure(c->chk, 8))
+      return 0;
+    HIP_TRY(hipMemsetAsync(c->chk.p, 0, 4, c->stream));
+    c->idx_chk = (uint32_t*)c->chk.p;
+  }
+  auto verified = [&]() -> int {
+    if (!c->idx_chk)
+      return 1;
+    uint32_t bad = 0;
+    c->idx_chk = nullptr;
+    HIP_TRY(hipMemcpyAsync(&bad, c->chk.p, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (bad)
+      *stale = true;
+    return 1;
+  };
   const uint64_t avail = capacity_words > W0 ? capacity_words - W0 : 0;
   uint64_t nwords;
   if (p.fixed)
@@ -1747,7 +1783,11 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
       t_timing.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
       t_timing.kernel_ms = 0;
       t_timing.timed = ok != 0;
-      return ok;
+      if (!ok) {
+        c->idx_chk = nullptr;
+        return 0;
+      }
+      return verified();
     }
   }
   HIP_TRY(hipEventRecord(c->ev[0], c->stream));
@@ -1778,15 +1818,47 @@ int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t*
     using S = std::remove_pointer_t<decltype(tag)>;
     return launch_decode<S>(c, p, (S*)d_field, d_in, nwords, g0, index);
   });
-  if (!ok)
+  if (!ok) {
+    c->idx_chk = nullptr;
     return 0;
+  }
   if (!dev_field && !copy_box(c, p, field_base, d_img, es, true))
     return 0;
   HIP_TRY(hipEventRecord(c->ev[3], c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   record_timing(c);
   *end_bit = bit_offset + total;
-  return 1;
+  return verified();
+}
+
+int zfp_hip_decompress(const zfp_hip_job* job, void* field_base, const uint64_t* words, uint64_t capacity_words,
+                       uint64_t bit_offset, int device, const zfp_hip_index* index, uint64_t* end_bit)
+{
+  Plan p;
+  if (!plan_job(job, field_base, p))
+    return 0;
+  if (!field_base || !words)
+    return fail("zfp_hip_decompress: null field or stream pointer");
+  if (zfp_hip_device_count() <= 0)
+    return fail("zfp_hip_decompress: no HIP device available");
+  CtxLease lease(device);
+  Ctx* c = lease.c;
+  if (!c)
+    return 0;
+  t_timing = Timing{};
+  if (p.g.nblocks == 0) {
+    *end_bit = bit_offset;
+    return 1;
+  }
+  bool stale = false;
+  int ok = decompress_once(c, p, job, field_base, words, capacity_words, bit_offset, index, end_bit, &stale);
+  if (ok && stale) {
+    // the caller's index passed the fingerprint but not the block lengths:
+    // decode again with the block starts found by the scan
+    ok = decompress_once(c, p, job, field_base, words, capacity_words, bit_offset, nullptr, end_bit, &stale);
+    t_timing.stale_index = true;
+  }
+  return ok;
 }
 
 int zfp_hip_index_build(const zfp_hip_job* job, const uint64_t* words, uint64_t capacity_words, uint64_t bit_offset,
@@ -1923,6 +1995,8 @@ int zfp_hip_last_timing(double* kernel_ms, double* total_ms)
   if (total_ms) *total_ms = t_timing.total_ms;
   return 1;
 }
+
+int zfp_hip_last_stale_index(void) { return t_timing.stale_index ? 1 : 0; }
 
 int zfp_hip_last_scan(double* scan_ms, int* passes)
 {

@@ -266,6 +266,7 @@ void zfp_chunks_free(zfp_chunks* chunks);
 zfp_blocks* zfp_blocks_alloc(void);
 void zfp_alloc_nblocks(zfp_blocks* blocks, const size_t nblocks);
 void zfp_blocks_free(zfp_blocks* blocks);
+zfp_blocks* zfp_blocks_alloc_beg(const size_t nchunks, const size_t* begs);
 void zfp_set_chunk_1d(zfp_chunk* chunk, const int fx, const int ex);
 void zfp_set_chunk_2d(zfp_chunk* chunk, const int fx, const int fy, const int ex, const int ey);
 void zfp_set_chunk_3d(zfp_chunk* chunk, const int fx, const int fy, const int fz, const int ex, const int ey, const int ez);
@@ -284,6 +285,12 @@ size_t zfp_compress(zfp_stream* stream, const zfp_field* field);
 size_t zfp_compress_chunk(zfp_stream* stream, const zfp_chunk* chunk, const zfp_field* field);
 size_t zfp_decompress(zfp_stream* stream, zfp_field* field);
 size_t zfp_decompress_chunk(zfp_stream* stream, const zfp_chunk* chunk, zfp_field* field);
+/* zfp.h:797-838: dispatch with an explicit execution policy, strided flag,
+ * dimensionality and scalar type (zfp_compress_chunk derives them) */
+size_t zfp_compress_call(zfp_stream* stream, const zfp_chunk* chunk, const zfp_field* field, const uint exec,
+                         const uint strided, const uint dims, const uint type);
+size_t zfp_decompress_call(zfp_stream* stream, const zfp_chunk* chunk, zfp_field* field, const uint exec,
+                           const uint strided, const uint dims, const uint type);
 size_t zfp_write_header(zfp_stream* stream, const zfp_field* field, uint mask);
 size_t zfp_read_header(zfp_stream* stream, zfp_field* field, uint mask);
 
@@ -308,6 +315,148 @@ size_t zfp_blocks_decompress(zfp_stream* stream, zfp_field* field, const int nth
 size_t zfp_blocks_decompress_multi_stream(zfp_stream* stream, zfp_field* field, zfp_streams* streams,
                                           const int nthreads);
 size_t zfp_blocks_decompress_single_stream(zfp_stream* stream, zfp_field* field, const int nthreads);
+
+/* ---- low-level block API (zfp.h:911-1061): one block per call, run on the GPU ---- */
+/* Each call codes one block at the stream's current bit position and leaves the
+ * stream positioned after it (not flushed), returning the bits written / read.
+ * A block is a field of at most 4 values per axis; partial blocks are padded
+ * as at a field's edge (encode.c:9-27).  Every call is a GPU call. */
+size_t zfp_encode_block_int32_1(zfp_stream* stream, const int32* block);
+size_t zfp_encode_block_int64_1(zfp_stream* stream, const int64* block);
+size_t zfp_encode_block_float_1(zfp_stream* stream, const float* block);
+size_t zfp_encode_block_double_1(zfp_stream* stream, const double* block);
+size_t zfp_encode_block_strided_int32_1(zfp_stream* stream, const int32* p, ptrdiff_t sx);
+size_t zfp_encode_block_strided_int64_1(zfp_stream* stream, const int64* p, ptrdiff_t sx);
+size_t zfp_encode_block_strided_float_1(zfp_stream* stream, const float* p, ptrdiff_t sx);
+size_t zfp_encode_block_strided_double_1(zfp_stream* stream, const double* p, ptrdiff_t sx);
+size_t zfp_encode_partial_block_strided_int32_1(zfp_stream* stream, const int32* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_encode_partial_block_strided_int64_1(zfp_stream* stream, const int64* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_encode_partial_block_strided_float_1(zfp_stream* stream, const float* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_encode_partial_block_strided_double_1(zfp_stream* stream, const double* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_encode_block_int32_2(zfp_stream* stream, const int32* block);
+size_t zfp_encode_block_int64_2(zfp_stream* stream, const int64* block);
+size_t zfp_encode_block_float_2(zfp_stream* stream, const float* block);
+size_t zfp_encode_block_double_2(zfp_stream* stream, const double* block);
+size_t zfp_encode_block_strided_int32_2(zfp_stream* stream, const int32* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_block_strided_int64_2(zfp_stream* stream, const int64* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_block_strided_float_2(zfp_stream* stream, const float* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_block_strided_double_2(zfp_stream* stream, const double* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_partial_block_strided_int32_2(zfp_stream* stream, const int32* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_partial_block_strided_int64_2(zfp_stream* stream, const int64* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_partial_block_strided_float_2(zfp_stream* stream, const float* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_partial_block_strided_double_2(zfp_stream* stream, const double* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_encode_block_int32_3(zfp_stream* stream, const int32* block);
+size_t zfp_encode_block_int64_3(zfp_stream* stream, const int64* block);
+size_t zfp_encode_block_float_3(zfp_stream* stream, const float* block);
+size_t zfp_encode_block_double_3(zfp_stream* stream, const double* block);
+size_t zfp_encode_block_strided_int32_3(zfp_stream* stream, const int32* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_block_strided_int64_3(zfp_stream* stream, const int64* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_block_strided_float_3(zfp_stream* stream, const float* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_block_strided_double_3(zfp_stream* stream, const double* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_partial_block_strided_int32_3(zfp_stream* stream, const int32* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_partial_block_strided_int64_3(zfp_stream* stream, const int64* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_partial_block_strided_float_3(zfp_stream* stream, const float* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_partial_block_strided_double_3(zfp_stream* stream, const double* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_encode_block_int32_4(zfp_stream* stream, const int32* block);
+size_t zfp_encode_block_int64_4(zfp_stream* stream, const int64* block);
+size_t zfp_encode_block_float_4(zfp_stream* stream, const float* block);
+size_t zfp_encode_block_double_4(zfp_stream* stream, const double* block);
+size_t zfp_encode_block_strided_int32_4(zfp_stream* stream, const int32* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_encode_block_strided_int64_4(zfp_stream* stream, const int64* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_encode_block_strided_float_4(zfp_stream* stream, const float* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_encode_block_strided_double_4(zfp_stream* stream, const double* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_encode_partial_block_strided_int32_4(zfp_stream* stream, const int32* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_encode_partial_block_strided_int64_4(zfp_stream* stream, const int64* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_encode_partial_block_strided_float_4(zfp_stream* stream, const float* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_encode_partial_block_strided_double_4(zfp_stream* stream, const double* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_block_int32_1(zfp_stream* stream, int32* block);
+size_t zfp_decode_block_int64_1(zfp_stream* stream, int64* block);
+size_t zfp_decode_block_float_1(zfp_stream* stream, float* block);
+size_t zfp_decode_block_double_1(zfp_stream* stream, double* block);
+size_t zfp_decode_block_strided_int32_1(zfp_stream* stream, int32* p, ptrdiff_t sx);
+size_t zfp_decode_block_strided_int64_1(zfp_stream* stream, int64* p, ptrdiff_t sx);
+size_t zfp_decode_block_strided_float_1(zfp_stream* stream, float* p, ptrdiff_t sx);
+size_t zfp_decode_block_strided_double_1(zfp_stream* stream, double* p, ptrdiff_t sx);
+size_t zfp_decode_partial_block_strided_int32_1(zfp_stream* stream, int32* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_decode_partial_block_strided_int64_1(zfp_stream* stream, int64* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_decode_partial_block_strided_float_1(zfp_stream* stream, float* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_decode_partial_block_strided_double_1(zfp_stream* stream, double* p, size_t nx,
+                                              ptrdiff_t sx);
+size_t zfp_decode_block_int32_2(zfp_stream* stream, int32* block);
+size_t zfp_decode_block_int64_2(zfp_stream* stream, int64* block);
+size_t zfp_decode_block_float_2(zfp_stream* stream, float* block);
+size_t zfp_decode_block_double_2(zfp_stream* stream, double* block);
+size_t zfp_decode_block_strided_int32_2(zfp_stream* stream, int32* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_block_strided_int64_2(zfp_stream* stream, int64* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_block_strided_float_2(zfp_stream* stream, float* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_block_strided_double_2(zfp_stream* stream, double* p, ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_partial_block_strided_int32_2(zfp_stream* stream, int32* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_partial_block_strided_int64_2(zfp_stream* stream, int64* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_partial_block_strided_float_2(zfp_stream* stream, float* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_partial_block_strided_double_2(zfp_stream* stream, double* p, size_t nx, size_t ny,
+                                              ptrdiff_t sx, ptrdiff_t sy);
+size_t zfp_decode_block_int32_3(zfp_stream* stream, int32* block);
+size_t zfp_decode_block_int64_3(zfp_stream* stream, int64* block);
+size_t zfp_decode_block_float_3(zfp_stream* stream, float* block);
+size_t zfp_decode_block_double_3(zfp_stream* stream, double* block);
+size_t zfp_decode_block_strided_int32_3(zfp_stream* stream, int32* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_block_strided_int64_3(zfp_stream* stream, int64* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_block_strided_float_3(zfp_stream* stream, float* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_block_strided_double_3(zfp_stream* stream, double* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_partial_block_strided_int32_3(zfp_stream* stream, int32* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_partial_block_strided_int64_3(zfp_stream* stream, int64* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_partial_block_strided_float_3(zfp_stream* stream, float* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_partial_block_strided_double_3(zfp_stream* stream, double* p, size_t nx, size_t ny, size_t nz,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz);
+size_t zfp_decode_block_int32_4(zfp_stream* stream, int32* block);
+size_t zfp_decode_block_int64_4(zfp_stream* stream, int64* block);
+size_t zfp_decode_block_float_4(zfp_stream* stream, float* block);
+size_t zfp_decode_block_double_4(zfp_stream* stream, double* block);
+size_t zfp_decode_block_strided_int32_4(zfp_stream* stream, int32* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_block_strided_int64_4(zfp_stream* stream, int64* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_block_strided_float_4(zfp_stream* stream, float* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_block_strided_double_4(zfp_stream* stream, double* p, ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_partial_block_strided_int32_4(zfp_stream* stream, int32* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_partial_block_strided_int64_4(zfp_stream* stream, int64* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_partial_block_strided_float_4(zfp_stream* stream, float* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+size_t zfp_decode_partial_block_strided_double_4(zfp_stream* stream, double* p, size_t nx, size_t ny, size_t nz, size_t nw,
+                                              ptrdiff_t sx, ptrdiff_t sy, ptrdiff_t sz, ptrdiff_t sw);
+void zfp_promote_int8_to_int32(int32* oblock, const int8* iblock, uint dims);
+void zfp_promote_uint8_to_int32(int32* oblock, const uint8* iblock, uint dims);
+void zfp_promote_int16_to_int32(int32* oblock, const int16* iblock, uint dims);
+void zfp_promote_uint16_to_int32(int32* oblock, const uint16* iblock, uint dims);
+void zfp_demote_int32_to_int8(int8* oblock, const int32* iblock, uint dims);
+void zfp_demote_int32_to_uint8(uint8* oblock, const int32* iblock, uint dims);
+void zfp_demote_int32_to_int16(int16* oblock, const int32* iblock, uint dims);
+void zfp_demote_int32_to_uint16(uint16* oblock, const int32* iblock, uint dims);
 
 #ifdef __cplusplus
 }

@@ -116,7 +116,9 @@ class ZfpCAPI:
         self.path = path
         self.lib = ctypes.CDLL(path)
         for name, (res, args) in self._SIGS.items():
-            fn = getattr(self.lib, name)
+            fn = getattr(self.lib, name, None)
+            if fn is None:  # an older library build (A/B timing tools); tests need every symbol
+                continue
             fn.restype = res
             fn.argtypes = args
 
@@ -167,7 +169,9 @@ class ZfpCAPI:
                                 ("zfp_hip_last_scan", i32, [vp, vp]), ("zfp_hip_scratch_bytes", sz, []),
                                 ("zfp_hip_release_scratch", i32, []), ("zfp_hip_last_stale_index", i32, []),
                                 ("zfp_hip_index_export", sz, [vp, vp, sz]), ("zfp_hip_index_import", vp, [vp, sz])]:
-            fn = getattr(self.lib, name)
+            fn = getattr(self.lib, name, None)
+            if fn is None:  # an older library build (A/B timing tools); tests need every symbol
+                continue
             fn.restype = res
             fn.argtypes = args
         self.keep_index = True

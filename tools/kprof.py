@@ -112,7 +112,10 @@ def main():
             k, t = ctypes.c_double(), ctypes.c_double()
             lib.zfp_hip_last_timing(ctypes.byref(k), ctypes.byref(t))
             ks.append(t.value if a.host else k.value)
-        print(("host->host call " if a.host else "") + "decode kernel_ms=%s  GB/s=%.1f" % (" ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3)))
+        sm, sp = ctypes.c_double(), ctypes.c_int()
+        scanned = lib.zfp_hip_last_scan(ctypes.byref(sm), ctypes.byref(sp))
+        print(("host->host call " if a.host else "") + "decode kernel_ms=%s  GB/s=%.1f  stale_index=%d scan=%d"
+              % (" ".join("%.3f" % x for x in ks), gb / (min(ks) * 1e-3), lib.zfp_hip_last_stale_index() if hasattr(lib, 'zfp_hip_last_stale_index') else -1, scanned))
 
 
 if __name__ == "__main__":

@@ -82,23 +82,20 @@ def profile_compress(zp, a):
             f = getattr(self._l, nm)
             return timed(nm, f) if nm in ("zfp_compress_chunk", "zfp_write_header", "stream_open") else f
 
-    saved = (zfpy_c._lib, zfpy_c._stream_bytes, zfpy_c._export_index, zfpy_c.compress_numpy_portion)
+    saved = (zfpy_c._lib, zfpy_c._bytes_from, zfpy_c._export_index)
     zfpy_c._lib = Lib(saved[0])
-    zfpy_c._stream_bytes = timed("stream_bytes", saved[1])
+    zfpy_c._bytes_from = timed("bytes_from", saved[1])
     zfpy_c._export_index = timed("export_index", saved[2])
-    zfpy_c.compress_numpy_portion = timed("portion", saved[3])
     import zfpy._zfp_par as zpar
-    saved_p = getattr(zpar, "compress_numpy_portion", None)
-    if saved_p is not None:
-        zpar.compress_numpy_portion = zfpy_c.compress_numpy_portion
+    saved_p = zpar._compress_portion
+    zpar._compress_portion = timed("portion", saved_p)
     try:
         t0 = time.perf_counter()
         zp.compress(nthreads=a.threads, rate=a.rate)
         t1 = time.perf_counter()
     finally:
-        zfpy_c._lib, zfpy_c._stream_bytes, zfpy_c._export_index, zfpy_c.compress_numpy_portion = saved
-        if saved_p is not None:
-            zpar.compress_numpy_portion = saved_p
+        zfpy_c._lib, zfpy_c._bytes_from, zfpy_c._export_index = saved
+        zpar._compress_portion = saved_p
     print("profile: compress wall %.1f ms" % (1e3 * (t1 - t0)))
     for nm, v in sorted(rec.items()):
         d = [1e3 * (b - x) for x, b in v]

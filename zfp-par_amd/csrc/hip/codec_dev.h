@@ -98,13 +98,7 @@ __device__ __forceinline__ uint32_t ctz64(uint64_t x)
 // land in spare words at the slot's end (sized by slot_words_for) that are
 // never read; readers mask at the block length.
 // ---------------------------------------------------------------------------
-// ZFP_EXP_PLAIN_STORE (timing experiments only, wrong output): plain stores in
-// place of the LDS ORs, to price the atomics
-#if ZFP_EXP_PLAIN_STORE
-#define ZFP_LDS_OR(p, v) (void)(*(p) = (v))
-#else
 #define ZFP_LDS_OR(p, v) (void)__hip_atomic_fetch_or((p), (v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)
-#endif
 __device__ __forceinline__ void lds_or32(uint32_t* p, uint32_t v)
 {
   ZFP_LDS_OR(p, v);

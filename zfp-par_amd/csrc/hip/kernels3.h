@@ -70,13 +70,6 @@ __device__ __forceinline__ uint32_t div_magic(uint32_t i, uint32_t m) { return m
 __host__ __device__ constexpr uint32_t slot_dwords_for(uint32_t lim) { return (lim + 95u) / 32u + 1u; }
 
 // (ZFP_NT_STORE, block3.h: the stream is written once and not read back)
-// wave priority while issuing the field loads / the copy-out (0: unchanged)
-#ifndef ZFP_ENC_PRIO
-#define ZFP_ENC_PRIO 0
-#endif
-#ifndef ZFP_ENC_PRIO_OUT
-#define ZFP_ENC_PRIO_OUT 0
-#endif
 
 template <typename S, bool VEC, bool REV, int WPG = kWavesPerGroup>
 __global__ __launch_bounds__(64 * WPG, 3) void encode3_aligned(const S* __restrict__ data, Geometry g, CodecParams cp,
@@ -89,15 +82,7 @@ __global__ __launch_bounds__(64 * WPG, 3) void encode3_aligned(const S* __restri
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   uint32_t* wslot = ldsw + (size_t)wv * 64 * sdw;
-#if ZFP_EXP_XCD_REMAP
-  // experiment: workgroup i runs on XCD i % 8; give each XCD a contiguous
-  // eighth of the field
-  const uint32_t nwg = gridDim.x;
-  const uint32_t bid = (nwg & 7u) ? blockIdx.x : (blockIdx.x & 7u) * (nwg >> 3) + (blockIdx.x >> 3);
-#else
-  const uint32_t bid = blockIdx.x;
-#endif
-  const uint64_t w = (uint64_t)bid * WPG + wv;
+  const uint64_t w = (uint64_t)blockIdx.x * WPG + wv;
   const uint64_t first = w * 64;
   const uint64_t b = first + lane;
   // the block loads are in flight while the wave copies the coder tables from
@@ -105,16 +90,10 @@ __global__ __launch_bounds__(64 * WPG, 3) void encode3_aligned(const S* __restri
   // tables, so no workgroup barrier is needed
   S v[64];
   BlockPos p{};
-#if ZFP_ENC_PRIO
-  __builtin_amdgcn_s_setprio(ZFP_ENC_PRIO);  // issue the loads ahead of the coding waves
-#endif
   if (b < g.nblocks) {
     p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
   }
-#if ZFP_ENC_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   {
     const uint4* src = reinterpret_cast<const uint4*>(&kCoderTables);
     uint4* dst = reinterpret_cast<uint4*>(lut);
@@ -135,9 +114,6 @@ __global__ __launch_bounds__(64 * WPG, 3) void encode3_aligned(const S* __restri
   // slots are read across lanes of this wave only: LDS ops of a wave complete in order
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
-#if ZFP_ENC_PRIO_OUT
-  __builtin_amdgcn_s_setprio(ZFP_ENC_PRIO_OUT);
-#endif
   const uint64_t nb = (g.nblocks - first) < 64 ? (g.nblocks - first) : 64;
   const uint32_t total = (uint32_t)nb * sw;  // run length in words
   uint64_t* dst = out + first * sw;
@@ -427,10 +403,6 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t x)
 // lane of the wave with the same arguments.
 __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
 {
-#ifdef ZFP_LB_FAKE
-  // experiment builds only: no waiting (wrong stream, inside the buffer) -- the look-back's cost
-  return w * (uint64_t)agg;
-#endif
   const uint32_t lane = threadIdx.x & 63u;
   if (w == 0) {
     if (lane == 0)
@@ -868,6 +840,9 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
       used = decode_block_n<S, D, REV>(r, sq, v, cp);
       scatter_n<S, D>(v, data, g, p);
     }
+    // (every decoder, the short-slot f64 one included: there the check costs
+    // about 12 % -- C3 decode 4.94 -> 5.54 ms, measured the same with the
+    // reader position, a cold call or the length parked in LDS)
     if (a.idx_bad && used != len)
       atomicOr(a.idx_bad, 1u);
   };

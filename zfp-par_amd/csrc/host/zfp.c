@@ -760,6 +760,19 @@ void zfp_alloc_nblocks(zfp_blocks* blocks, const size_t nblocks)
   blocks->begs = (size_t*)calloc(nblocks + 1, sizeof(size_t));
 }
 
+/* zfp.c:141-147 (exported, not declared in the reference header): a
+ * partition record holding nchunks + 1 given chunk offsets */
+zfp_blocks* zfp_blocks_alloc_beg(const size_t nchunks, const size_t* begs)
+{
+  zfp_blocks* blocks = zfp_blocks_alloc();
+  if (!blocks)
+    return NULL;
+  zfp_alloc_nblocks(blocks, nchunks);
+  if (blocks->begs && begs)
+    memcpy(blocks->begs, begs, sizeof(size_t) * (nchunks + 1));
+  return blocks;
+}
+
 void zfp_blocks_free(zfp_blocks* blocks)
 {
   if (!blocks)
@@ -1016,7 +1029,39 @@ size_t zfp_compress(zfp_stream* zfp, const zfp_field* field)
   return zfp_compress_chunk(zfp, &whole, field);
 }
 
+static size_t compress_exec(zfp_stream* zfp, const zfp_chunk* chunk, const zfp_field* field, uint exec);
+static size_t decompress_exec(zfp_stream* zfp, const zfp_chunk* chunk, zfp_field* field, uint exec);
+
 size_t zfp_compress_chunk(zfp_stream* zfp, const zfp_chunk* chunk, const zfp_field* field)
+{
+  return compress_exec(zfp, chunk, field, (uint)zfp->exec.policy);
+}
+
+/* zfp.c:1510-1564: the reference's function-table dispatch with the execution
+ * policy, strided flag, dimensionality and scalar type given by the caller
+ * (zfp_compress_chunk derives them from the stream and field).  Here every
+ * serial/OpenMP entry is the GPU path; `strided` selects nothing (the kernels
+ * take strides either way); a type or dimensionality that disagrees with the
+ * field has no table entry in this library and returns 0. */
+size_t zfp_compress_call(zfp_stream* zfp, const zfp_chunk* chunk, const zfp_field* field, const uint exec,
+                         const uint strided, const uint dims, const uint type)
+{
+  (void)strided;
+  if (exec > (uint)zfp_exec_hip || dims != zfp_field_dimensionality(field) || type != (uint)field->type)
+    return 0;
+  return compress_exec(zfp, chunk, field, exec);
+}
+
+size_t zfp_decompress_call(zfp_stream* zfp, const zfp_chunk* chunk, zfp_field* field, const uint exec,
+                           const uint strided, const uint dims, const uint type)
+{
+  (void)strided;
+  if (exec > (uint)zfp_exec_hip || dims != zfp_field_dimensionality(field) || type != (uint)field->type)
+    return 0;
+  return decompress_exec(zfp, chunk, field, exec);
+}
+
+static size_t compress_exec(zfp_stream* zfp, const zfp_chunk* chunk, const zfp_field* field, uint exec)
 {
   bitstream* s = zfp->stream;
   zfp_hip_job job;
@@ -1032,9 +1077,9 @@ size_t zfp_compress_chunk(zfp_stream* zfp, const zfp_chunk* chunk, const zfp_fie
     default:
       return 0;
   }
-  if (zfp->exec.policy == zfp_exec_cuda)
+  if (exec == zfp_exec_cuda)
     return 0;
-  if (zfp->exec.policy == zfp_exec_omp) {
+  if (exec == zfp_exec_omp) {
     /* the reference's OpenMP compressor ignores the chunk (ompcompress.c:155-210) */
     whole.fx = whole.fy = whole.fz = whole.fw = 0;
     whole.ex = field->nx;
@@ -1080,6 +1125,11 @@ size_t zfp_decompress(zfp_stream* zfp, zfp_field* field)
 
 size_t zfp_decompress_chunk(zfp_stream* zfp, const zfp_chunk* chunk, zfp_field* field)
 {
+  return decompress_exec(zfp, chunk, field, (uint)zfp->exec.policy);
+}
+
+static size_t decompress_exec(zfp_stream* zfp, const zfp_chunk* chunk, zfp_field* field, uint exec)
+{
   bitstream* s = zfp->stream;
   zfp_hip_job job;
   uint64 end = 0;
@@ -1094,7 +1144,7 @@ size_t zfp_decompress_chunk(zfp_stream* zfp, const zfp_chunk* chunk, zfp_field* 
       return 0;
   }
   /* no OpenMP or CUDA decompressor in the reference table (zfp.c:1623-1637) */
-  if (zfp->exec.policy == zfp_exec_omp || zfp->exec.policy == zfp_exec_cuda)
+  if (exec == zfp_exec_omp || exec == zfp_exec_cuda)
     return 0;
   job_from(&job, zfp, chunk, field);
   if (variable_rate(zfp, field)) {
@@ -1111,6 +1161,56 @@ size_t zfp_decompress_chunk(zfp_stream* zfp, const zfp_chunk* chunk, zfp_field* 
   s->bits = 0;
   s->buffer = 0;
   return stream_size(s);
+}
+
+/* One block of the low-level API (encode.c / decode.c templates: zfp_encode_
+ * block_*, zfp_decode_block_*): the same GPU call as a chunk, on a field that
+ * is the block, at the stream's bit position -- pending bits of a partly
+ * written word included -- and with no flush, so consecutive blocks are packed
+ * bit after bit as by the reference's serial coder.  Variable-rate blocks are
+ * decoded with the index scan of that one block. */
+size_t zfp_block_code(zfp_stream* zfp, zfp_type type, uint dims, void* p, const size_t* n, const ptrdiff_t* st,
+                      int decode)
+{
+  bitstream* s = zfp->stream;
+  zfp_field f;
+  zfp_chunk box;
+  zfp_hip_job job;
+  uint64 start, end = 0;
+  size_t* nn[4] = {&f.nx, &f.ny, &f.nz, &f.nw};
+  ptrdiff_t* ss[4] = {&f.sx, &f.sy, &f.sz, &f.sw};
+  size_t* bf[4] = {&box.fx, &box.fy, &box.fz, &box.fw};
+  size_t* be[4] = {&box.ex, &box.ey, &box.ez, &box.ew};
+  memset(&f, 0, sizeof f);
+  f.type = type;
+  f.data = p;
+  for (uint a = 0; a < 4; a++) {
+    *nn[a] = a < dims ? n[a] : 0;
+    *ss[a] = a < dims ? st[a] : 0;
+    *bf[a] = 0;
+    *be[a] = a < dims ? n[a] : 0;
+  }
+  for (uint a = 0; a < dims; a++)
+    if (n[a] < 1 || n[a] > 4)
+      return 0;
+  job_from(&job, zfp, &box, &f);
+  if (!decode) {
+    start = stream_wtell(s);
+    if (!zfp_hip_compress(&job, p, s->begin, (uint64)(s->end - s->begin), start, s->buffer, stream_device(zfp), NULL,
+                          &end)) {
+      report("zfp_encode_block");
+      return 0;
+    }
+    stream_wseek(s, end);
+  } else {
+    start = stream_rtell(s);
+    if (!zfp_hip_decompress(&job, p, s->begin, (uint64)(s->end - s->begin), start, stream_device(zfp), NULL, &end)) {
+      report("zfp_decode_block");
+      return 0;
+    }
+    stream_rseek(s, end);
+  }
+  return (size_t)(end - start);
 }
 
 /* ------------------------------------------------------------------------ */

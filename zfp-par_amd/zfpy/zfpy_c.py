@@ -162,7 +162,9 @@ class ZfpBytes(bytes):
 _tls = threading.local()
 _KEEP_OUT_MAX = 256 << 20
 
-_bytes_uninit = ctypes.pythonapi.PyBytes_FromStringAndSize
+# (indexing makes a function object of its own: attribute access returns one
+# shared object, whose restype the second binding below would overwrite)
+_bytes_uninit = ctypes.pythonapi["PyBytes_FromStringAndSize"]
 _bytes_uninit.restype = ctypes.py_object
 _bytes_uninit.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
 
@@ -175,6 +177,43 @@ def _out_buffer(size):
     if a.size <= _KEEP_OUT_MAX:
         _tls.out = a
     return a, a.ctypes.data
+
+
+_bytes_raw = ctypes.pythonapi["PyBytes_FromStringAndSize"]
+_bytes_raw.restype = ctypes.c_void_p
+_bytes_raw.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+_bytes_resize = ctypes.pythonapi._PyBytes_Resize
+_bytes_resize.restype = ctypes.c_int
+_bytes_resize.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_ssize_t]
+_py_decref = ctypes.pythonapi.Py_DecRef
+_py_decref.restype = None
+_py_decref.argtypes = [ctypes.c_void_p]
+_bytes_data_offset = bytes.__basicsize__ - 1  # ob_sval: the bytes' storage after the header
+
+
+def _bytes_target(size):
+    """(handle, address): a new, not yet shared bytes object of `size` bytes
+    that the library writes the stream into directly (no staging buffer, no
+    copy afterwards).  The handle owns the only reference; _bytes_take or
+    _bytes_drop must consume it."""
+    h = _bytes_raw(None, max(size, 1))
+    if not h:
+        raise MemoryError("bytes of %d" % size)
+    return h, h + _bytes_data_offset
+
+
+def _bytes_take(h, n):
+    """The bytes object of handle h, shrunk to its first n bytes."""
+    ref = ctypes.c_void_p(h)
+    if _bytes_resize(ctypes.byref(ref), n) != 0:  # frees the object on failure
+        raise MemoryError("bytes resize to %d" % n)
+    out = ctypes.cast(ref, ctypes.py_object).value  # + 1 reference
+    _py_decref(ref)
+    return out
+
+
+def _bytes_drop(h):
+    _py_decref(h)
 
 
 def _bytes_from(addr, n):
@@ -518,13 +557,17 @@ def _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision,
     field = _init_field_raw(py_raw_array, chunkit)
     stream = _lib.zfp_stream_open(None)
     bstream = None
+    target = None
     try:
         if device >= 0:
             _lib.zfp_stream_set_hip_device(stream, device)
         _set_compression_mode(stream, type_none, chunkit.ndim, tolerance, rate, precision)
         ck = chunkit.chunk_ptr(ichunk)
         maxsize = _lib.zfp_stream_maximum_size_chunk(stream, field, ck) + (HEADER_MAX_BITS + 63) // 64 * 8 + 8
-        obuf, buf = _out_buffer(maxsize)
+        if plain:
+            target, buf = _bytes_target(maxsize)
+        else:
+            obuf, buf = _out_buffer(maxsize)
         bstream = _lib.stream_open(buf, maxsize)
         _lib.zfp_stream_set_bit_stream(stream, bstream)
         _lib.zfp_stream_rewind(stream)
@@ -535,9 +578,12 @@ def _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision,
             raise RuntimeError("Failed to write to stream")
         blob = _export_index(stream)
         if plain:
-            return _bytes_from(buf, n), blob
+            out, target = _bytes_take(target, n), None
+            return out, blob
         return _stream_bytes(obuf, n, blob)
     finally:
+        if target is not None:
+            _bytes_drop(target)
         _lib.zfp_field_free(field)
         _lib.zfp_stream_close(stream)
         if bstream:

@@ -1060,6 +1060,15 @@ __device__ __forceinline__ uint32_t squeeze32(const uint32_t* sq, uint32_t f)
 #else
 #define ZFP_DP64_ATTR __forceinline__
 #endif
+// Rare wave-uniform branches of the decoder, laid out after the hot path
+#ifndef ZFP_DEC_COLD
+#define ZFP_DEC_COLD 0
+#endif
+#if ZFP_DEC_COLD
+#define ZFP_RARE(x) __builtin_expect(!!(x), 0)
+#else
+#define ZFP_RARE(x) (x)
+#endif
 template <bool IMP = true, int SIZE = 64>
 __device__ ZFP_DP64_ATTR uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
 {
@@ -1096,12 +1105,12 @@ __device__ ZFP_DP64_ATTR uint64_t decode_plane64(WordReader& r, const uint32_t* 
   const uint64_t F = (fast || imp0) ? S & mq & (((S & ~se) & kEven) | ((S & ~so) & kOdd)) : 0ull;
   const uint32_t Fl = (uint32_t)F, Fh = (uint32_t)(F >> 32);
   uint64_t xx = squeeze32(sq, Fl);
-  if (__any(Fh != 0))  // some section reaches past stream bit 32
+  if (ZFP_RARE(__any(Fh != 0)))  // some section reaches past stream bit 32
     xx |= (uint64_t)squeeze32(sq, Fh) << (32u - (uint32_t)__popc(Fl));
   uint32_t k63 = 0, si = 0;
   uint64_t xi = 0;
   bool imp = false;
-  if (__any(imp0)) {  // wave-uniform: most planes have no such lane
+  if (ZFP_RARE(__any(imp0))) {  // wave-uniform: most planes have no such lane
     k63 = ((uint32_t)SIZE - 1 - n) & 63u;  // tokens below the last coefficient
     xi = xx & ((1ull << k63) - 1);
     si = k63 + (uint32_t)__popcll(xi);  // section bits of those tokens
@@ -1113,7 +1122,7 @@ __device__ ZFP_DP64_ATTR uint64_t decode_plane64(WordReader& r, const uint32_t* 
   r.pos = pos + used;
   bits = bl - used;
   const bool slow = grp && one && !fast && !imp;
-  if (__any(slow)) {
+  if (ZFP_RARE(__any(slow))) {
     if (slow)
       decode_group_slow<SIZE>(r, x, bits, n);
   }
@@ -1248,7 +1257,7 @@ __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_
 #if !ZFP_DEC32_SWITCH
     const bool slow = act && !fast;
     const uint64_t sm = __builtin_amdgcn_ballot_w64(slow);
-    if (sm != 0) {
+    if (ZFP_RARE(sm != 0)) {
       if (slow) {
         uint32_t b = bits;
         P[k] = decode_plane64<IMP>(r, sq, b, n);

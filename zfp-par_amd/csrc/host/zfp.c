@@ -1202,13 +1202,42 @@ size_t zfp_block_code(zfp_stream* zfp, zfp_type type, uint dims, void* p, const 
       return 0;
     }
     stream_wseek(s, end);
-  } else {
+  } else if (zfp_hip_is_device_ptr(p)) {
     start = stream_rtell(s);
     if (!zfp_hip_decompress(&job, p, s->begin, (uint64)(s->end - s->begin), start, stream_device(zfp), NULL, &end)) {
       report("zfp_decode_block");
       return 0;
     }
     stream_rseek(s, end);
+  } else {
+    /* decoded into a contiguous block here, then copied out with the caller's
+     * strides (a host field with any strides, as the reference's scatter) */
+    unsigned char tmp[256 * sizeof(double)];
+    const size_t es = zfp_type_size(type);
+    size_t m[4] = {1, 1, 1, 1};
+    ptrdiff_t cs[4] = {1, 0, 0, 0};
+    for (uint a = 0; a < dims; a++)
+      m[a] = n[a];
+    for (uint a = 1; a < dims; a++)
+      cs[a] = cs[a - 1] * (ptrdiff_t)n[a - 1];
+    f.data = tmp;
+    for (uint a = 0; a < 4; a++)
+      *ss[a] = a < dims ? cs[a] : 0;
+    job_from(&job, zfp, &box, &f);
+    start = stream_rtell(s);
+    if (!zfp_hip_decompress(&job, tmp, s->begin, (uint64)(s->end - s->begin), start, stream_device(zfp), NULL, &end)) {
+      report("zfp_decode_block");
+      return 0;
+    }
+    stream_rseek(s, end);
+    for (size_t l = 0; l < m[3]; l++)
+      for (size_t k = 0; k < m[2]; k++)
+        for (size_t j = 0; j < m[1]; j++)
+          for (size_t i = 0; i < m[0]; i++) {
+            const ptrdiff_t o = (ptrdiff_t)i * st[0] + (dims > 1 ? (ptrdiff_t)j * st[1] : 0) +
+                                (dims > 2 ? (ptrdiff_t)k * st[2] : 0) + (dims > 3 ? (ptrdiff_t)l * st[3] : 0);
+            memcpy((unsigned char*)p + o * (ptrdiff_t)es, tmp + (i + m[0] * (j + m[1] * (k + m[2] * l))) * es, es);
+          }
   }
   return (size_t)(end - start);
 }

@@ -191,6 +191,32 @@ _py_decref.argtypes = [ctypes.c_void_p]
 _bytes_data_offset = bytes.__basicsize__ - 1  # ob_sval: the bytes' storage after the header
 
 
+try:
+    _madvise = ctypes.CDLL(None, use_errno=True).madvise
+    _madvise.restype = ctypes.c_int
+    _madvise.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+except (OSError, AttributeError):  # not Linux/glibc: pages fault in as written
+    _madvise = None
+_MADV_HUGEPAGE, _MADV_POPULATE_WRITE = 14, 23
+_RESIDENT_MIN = 8 << 20
+
+
+def _make_resident(addr, size):
+    """Back a large new buffer with huge pages and fault them in here, in the
+    calling thread (outside the GIL: ctypes releases it).  Otherwise every 4 KB
+    page of a fresh stream faults inside the library's device-to-host copy:
+    zfp_parallel's eight 64 MB chunk streams took 74-83 ms to compress instead
+    of 54 ms (tools/exp/zpar_conc3.py, profiles/r4_zfp_parallel.txt).  Best
+    effort: kernels without MADV_POPULATE_WRITE (Linux < 5.14) or without
+    transparent huge pages ignore it."""
+    if _madvise is None or size < _RESIDENT_MIN:
+        return
+    lo = (addr + 4095) & ~4095
+    n = (addr + size - lo) & ~4095
+    _madvise(lo, n, _MADV_HUGEPAGE)
+    _madvise(lo, n, _MADV_POPULATE_WRITE)
+
+
 def _bytes_target(size):
     """(handle, address): a new, not yet shared bytes object of `size` bytes
     that the library writes the stream into directly (no staging buffer, no
@@ -199,6 +225,7 @@ def _bytes_target(size):
     h = _bytes_raw(None, max(size, 1))
     if not h:
         raise MemoryError("bytes of %d" % size)
+    _make_resident(h + _bytes_data_offset, size)
     return h, h + _bytes_data_offset
 
 

@@ -840,9 +840,9 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
       used = decode_block_n<S, D, REV>(r, sq, v, cp);
       scatter_n<S, D>(v, data, g, p);
     }
-    // (every decoder, the short-slot f64 one included: there the check costs
-    // about 12 % -- C3 decode 4.94 -> 5.54 ms, measured the same with the
-    // reader position, a cold call or the length parked in LDS)
+    // (every decoder, the short-slot f64 one included: at its register bound
+    // the check moved its spills into the plane loop, C3 decode 4.94 -> 5.54
+    // ms, until the rare branches were laid out cold: 4.84 ms, ZFP_RARE)
     if (a.idx_bad && used != len)
       atomicOr(a.idx_bad, 1u);
   };

@@ -479,7 +479,7 @@ __device__ __forceinline__ int lossy_emax_cast(int32_t (&q)[64], float (&v)[64],
 #pragma unroll
   for (int i = 0; i < 64; i++)
     q[i] = (int32_t)(s * v[i]);
-  if (ZFP_ENC_RARE(__any(cast && (bad || emax < -97)))) {
+  if (__any(cast && (bad || emax < -97))) {
     float w[64];
     reload(w);
     fwd_cast(q, w, emax);

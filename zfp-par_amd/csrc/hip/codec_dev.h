@@ -298,15 +298,6 @@ __device__ __forceinline__ void pin_registers(U (&a)[N])
 // per-block index check included); the f32 decoder's instruction-cache misses
 // 5.8 -> 3.7 per wave at the same time (profiles/r4m_cold_ab.txt)
 #define ZFP_RARE(x) __builtin_expect(!!(x), 0)
-#ifndef ZFP_ENC_COLD
-#define ZFP_ENC_COLD 0
-#endif
-#if ZFP_ENC_COLD
-#define ZFP_ENC_RARE(x) __builtin_expect(!!(x), 0)
-#else
-#define ZFP_ENC_RARE(x) (x)
-#endif
-
 // Bit reader over a word array in LDS (or global memory).
 struct WordReader {
   const uint64_t* w;
@@ -764,7 +755,7 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
       lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
       lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
     }
-    if (ZFP_ENC_RARE(__builtin_amdgcn_ballot_w64(ext) != 0)) {
+    if (__builtin_amdgcn_ballot_w64(ext) != 0) {
       const uint32_t g32 = (l1 << sh1) >> 31;  // bit 31 of d16: bit 32 of the plane's group bits
       const ExtEvent e{p31 - 31u + n, x0, (uint32_t)(xs >> 32), h | (impl << 6) | (g32 << 7)};
       if constexpr (PREC <= 32) {
@@ -808,7 +799,7 @@ __device__ __forceinline__ uint32_t code_planes(OrSlot& s, const uint32_t* lut, 
     nn = ~n;
   }
   if constexpr (PREC > 32) {
-    if (ZFP_ENC_RARE(__any(e0.hb >= 16u))) {
+    if (__any(e0.hb >= 16u)) {
       expand_event(s, lut, e0);
       if (__any(e1.hb >= 16u)) {
         expand_event(s, lut, e1);
@@ -908,7 +899,7 @@ __device__ __forceinline__ void code_planes_fru(OrSlot& os, const uint32_t* lut,
     uint32_t L = e1 - impl + 1u - (n1 >> 6);  // group bits: none once all 64 are significant
     const bool ext = x0 > 0xfffeu || x1 != 0u;
     const int32_t Qg = Q - (int32_t)n;
-    if (ZFP_ENC_RARE(__builtin_amdgcn_ballot_w64(ext) != 0)) {
+    if (__builtin_amdgcn_ballot_w64(ext) != 0) {
       // rare: xs reaches past unit 0 (or x0 == 0xffff); the other lanes take no part
       uint32_t hb = 0;
       if (ext) {
@@ -965,7 +956,7 @@ __device__ __forceinline__ void code_planes_fr32(uint32_t* slot, uint32_t jmax, 
         const uint32_t d = (l1 << (l0 & 31u)) | (l0 >> 5);  // (dbl(xs & 0xffff) << 1 | 1) mod 2^32
         uint32_t g = d - (1u << (e1 & 31u));
         const bool ext = xs > 0xfffeu;
-        if (ZFP_ENC_RARE(__builtin_amdgcn_ballot_w64(ext) != 0)) {
+        if (__builtin_amdgcn_ballot_w64(ext) != 0) {
           // rare: the lanes whose top one lies past unit 0 (or xs == 0xffff,
           // whose group bits are 33 long) have no surplus in unit 0; their
           // later units are written as in code_planes (bit 32 of the group

@@ -646,7 +646,7 @@ static int run_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out,
     if (swp < swp_full) {
       uint64_t cap = std::min<uint64_t>(p.g.nblocks, std::max<uint64_t>(16384, p.g.nblocks / 16));
       if (const char* e = getenv("ZFP_HIP_OVF_POOL"))
-        cap = std::max<uint64_t>(1, std::min<uint64_t>(cap, (uint64_t)atoll(e)));
+        cap = std::max<uint64_t>(1, std::min<uint64_t>(p.g.nblocks, (uint64_t)atoll(e)));
       if (!ensure(c->ovf, cap * sizeof(OvfEntry)))
         return 0;
       a.ovf = (uint64_t*)c->ovf.p;

@@ -590,15 +590,17 @@ static uint32_t short_slot_words(const Plan& p)
 // Short slots for the variable-rate 4D encoder (f32 fields): the region of 16
 // slots sized for the worst case (f32 reversible: 8,462 bits, 17.3 KB) limits
 // the CU to 8 one-wave workgroups (2 waves per SIMD), where the registers allow
-// 3 (f32 reversible) or 4 (f32 lossy).  Slots cut to what 12 waves per CU
-// leave (blocks that code longer go to encode4_patch) measured no faster on
-// 128^4 f32 reversible (1.56 ms either way, round 4), and on the C5 chunk
-// more than 1/16 of the blocks -- the ones that fail the reversible cast test,
-// about 8,300 bits each -- overflowed, so the overflow pool ran out and the
-// launch was repeated with full slots (46 -> 90 ms per call).  So full-size
-// slots by default; ZFP_HIP_SLOT_WORDS=n forces n-word slots (tests of the
-// overflow and patch path).  (Rounds 2-3 sized them by waves per SIMD instead
-// of per CU, which left them full-size as well.)
+// 3 (f32 reversible).  f32 reversible slots are cut to what 12 waves per CU
+// leave (93 words = 5,952 bits); a block that codes longer -- on the C5 field,
+// the blocks that fail the reversible cast test, about 8,300 bits each -- is
+// packed with its first bits and listed, and encode4_patch codes it again with
+// a full slot.  The overflow pool holds every block, so it cannot run out (the
+// round-4 first try sized it for 1/16 of them: more overflowed on C5 and the
+// launch was redone with full slots, 46 -> 90 ms).  C5 chunk 46.4 -> 43.1 ms;
+// 128^4 1.51 -> 1.55 ms (profiles/r4o_4d_slots.txt).  Lossy f32 modes keep
+// full slots (not measured).  ZFP_HIP_SLOT_WORDS=n forces n-word slots (tests
+// of the overflow and patch path), ZFP_HIP_FULL_SLOTS=1 full ones.
+constexpr uint32_t kShortSlotWords4 = 93;
 template <typename S>
 static uint32_t short_slot_words4(const Plan& p)
 {
@@ -606,7 +608,7 @@ static uint32_t short_slot_words4(const Plan& p)
     return ~0u;
   if (const char* e = getenv("ZFP_HIP_SLOT_WORDS"))  // tests: force overflows
     return (uint32_t)atoi(e) | 1u;
-  return ~0u;
+  return p.cp.minexp < kMinExp ? kShortSlotWords4 : ~0u;
 }
 
 template <typename S>
@@ -644,8 +646,8 @@ static int run_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out,
     if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
       return 0;
     if (swp < swp_full) {
-      uint64_t cap = std::min<uint64_t>(p.g.nblocks, std::max<uint64_t>(16384, p.g.nblocks / 16));
-      if (const char* e = getenv("ZFP_HIP_OVF_POOL"))
+      uint64_t cap = p.g.nblocks;  // every block may overflow: no redo
+      if (const char* e = getenv("ZFP_HIP_OVF_POOL"))  // tests: force the full-slot redo
         cap = std::max<uint64_t>(1, std::min<uint64_t>(p.g.nblocks, (uint64_t)atoll(e)));
       if (!ensure(c->ovf, cap * sizeof(OvfEntry)))
         return 0;

@@ -253,3 +253,25 @@ def test_zslab_chunk_payloads_concatenate_to_whole_stream(product, oracle):
         body = (w[1:1 + p] >> np.uint64(32)) | (w[2:2 + p] << np.uint64(32))
         bits += body.tobytes()
     assert bits == bytes(whole)
+
+
+@pytest.mark.gpu
+def test_large_calls_do_not_keep_their_stream_buffer(product, monkeypatch):
+    """the per-thread staging buffer of compress_numpy is
+    kept only up to zfpy_c._KEEP_OUT_MAX bytes; a call that needs more allocates
+    its own and drops it, so one huge call does not pin memory for the thread's
+    lifetime.  (Cap lowered here so a small field exceeds it.)"""
+    zc = zfpy.zfpy_c
+    monkeypatch.setattr(zc, "_KEEP_OUT_MAX", 1 << 20)
+    if hasattr(zc._tls, "out"):
+        monkeypatch.delattr(zc._tls, "out")
+    rng = np.random.default_rng(5)
+    small = rng.standard_normal((16, 16, 16)).astype(np.float32)
+    zfpy.compress_numpy(small, rate=8)
+    kept = getattr(zc._tls, "out", None)
+    assert kept is not None and kept.size <= 1 << 20
+    big = rng.standard_normal((64, 128, 128)).astype(np.float32)  # 4 MB stream bound at rate 32
+    s = zfpy.compress_numpy(big, rate=32)
+    assert getattr(zc._tls, "out", None) is kept, "a buffer above the cap must not replace the kept one"
+    back = zfpy.decompress_numpy(s)
+    assert back.shape == big.shape

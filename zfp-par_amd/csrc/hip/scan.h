@@ -42,17 +42,6 @@
 
 namespace zfp_amd {
 
-#ifndef ZFP_SCAN_COLD
-#define ZFP_SCAN_COLD 0
-#endif
-#if ZFP_SCAN_COLD
-#define ZFP_SCAN_RARE(x) __builtin_expect(!!(x), 0)
-#define ZFP_SCAN_LIKELY(x) __builtin_expect(!!(x), 1)
-#else
-#define ZFP_SCAN_RARE(x) (x)
-#define ZFP_SCAN_LIKELY(x) (x)
-#endif
-
 // ---------------------------------------------------------------------------
 // per-lane stream reader: ring of kRing words in LDS + kHalf prefetched words
 #ifndef ZFP_SCAN_RING_WORDS
@@ -163,7 +152,7 @@ __device__ __forceinline__ void scan_section(R& rd, uint64_t& p, uint32_t& bits,
         const uint64_t mq = (ends - 1) & ~ends;
         const uint32_t ones = (uint32_t)__popcll(S & mq);
         const uint32_t P = q - (ones - 1) / 2;
-        if (ZFP_SCAN_LIKELY(nn + P <= (uint32_t)SIZE - 1 && used + q + 1 <= bits)) {
+        if (nn + P <= (uint32_t)SIZE - 1 && used + q + 1 <= bits) {
           p = q0 + q + 1;
           bits -= used + q + 1;
           n = nn + P;
@@ -177,7 +166,7 @@ __device__ __forceinline__ void scan_section(R& rd, uint64_t& p, uint32_t& bits,
       const uint32_t c = avail - (run & 1u);
       const uint32_t ones = (uint32_t)__popcll(S & low_mask(c));  // even
       const uint32_t cnt = c - ones / 2;  // "0" tokens + "11" tokens
-      if (ZFP_SCAN_RARE(nn + cnt > (uint32_t)SIZE - 1 || used + c > bits))
+      if (nn + cnt > (uint32_t)SIZE - 1 || used + c > bits)
         break;
       nn += cnt;
       used += c;

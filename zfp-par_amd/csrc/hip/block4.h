@@ -368,9 +368,6 @@ __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, con
 // redundantly (same stream bits, same control flow), each lane keeping the
 // ones of its segment; verbatim bits are read per segment.  One iteration per
 // group test, i.e. per newly significant coefficient plus one per plane.
-#ifndef ZFP_DEC4_WIN
-#define ZFP_DEC4_WIN 0
-#endif
 template <int PREC>
 __device__ __forceinline__ uint32_t decode_planes4(WordReader& rd, uint32_t budget, uint32_t maxprec,
                                                    uint64_t (&P)[PREC])
@@ -394,55 +391,6 @@ __device__ __forceinline__ uint32_t decode_planes4(WordReader& rd, uint32_t budg
       uint64_t x = seg.read(cnt);
       rd.skip(m);
       bits -= m;
-#if ZFP_DEC4_WIN
-      // the group tests from a 128-bit register window (lo: the 64 stream
-      // bits from wpos, hi: the next 64) refilled with one LDS read per 64
-      // bits consumed, instead of two LDS round trips per test
-      if (n < 256u && bits) {
-        uint32_t wpos = rd.pos, off = 0;
-        uint64_t lo = rd.peek_at(wpos), hi = rd.peek_at(wpos + 64u);
-        auto cur = [&]() { return off ? (lo >> off) | (hi << (64u - off)) : lo; };
-        auto adv = [&](uint32_t t) {
-          off += t;
-          while (off >= 64u) {
-            off -= 64u;
-            wpos += 64u;
-            lo = hi;
-            hi = rd.peek_at(wpos + 64u);
-          }
-        };
-        while (n < 256u && bits) {
-          bits--;
-          const uint64_t w = cur();
-          adv(1u);
-          if (!(w & 1u))
-            break;
-          for (;;) {  // zeros up to the next one, at most to coefficient 255 / the budget
-            const uint32_t lim = min(255u - n, bits);
-            const uint32_t z = ctz64(cur());  // 64: no one in the next 64 bits
-            if (z >= lim) {
-              adv(lim);
-              bits -= lim;
-              n += lim;
-              break;
-            }
-            if (z < 64u) {
-              adv(z + 1u);
-              bits -= z + 1u;
-              n += z;
-              break;
-            }
-            adv(64u);
-            bits -= 64u;
-            n += 64u;
-          }
-          if (n - base < 64u)
-            x |= 1ull << (n - base);
-          n++;
-        }
-        rd.pos = wpos + off;
-      }
-#else
       while (n < 256u && bits) {
         bits--;
         if (!rd.read1())
@@ -470,7 +418,6 @@ __device__ __forceinline__ uint32_t decode_planes4(WordReader& rd, uint32_t budg
           x |= 1ull << (n - base);
         n++;
       }
-#endif
       P[k] = x;
     }
   }

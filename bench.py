@@ -227,7 +227,8 @@ def main():
     if distributed:
         dist.init_process_group("nccl", device_id=dev)
 
-    api = load_capi(os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so"))
+    # ZFP_BENCH_LIB: a variant build for A/B timing (tools/exp); the product library otherwise
+    api = load_capi(os.environ.get("ZFP_BENCH_LIB") or os.path.join(REPO, "zfp-par_amd", "lib", "libzfp.so"))
     api.enable_index()
     lib = api.lib
     lib.zfp_hip_last_timing.argtypes = [ctypes.c_void_p, ctypes.c_void_p]

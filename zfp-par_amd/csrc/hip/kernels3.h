@@ -90,10 +90,19 @@ __global__ __launch_bounds__(64 * WPG, 3) void encode3_aligned(const S* __restri
   // tables, so no workgroup barrier is needed
   S v[64];
   BlockPos p{};
+#ifndef ZFP_ALIGNED_PRIO
+#define ZFP_ALIGNED_PRIO 0
+#endif
+#if ZFP_ALIGNED_PRIO
+  __builtin_amdgcn_s_setprio(1);  // the block loads go out ahead of the coding waves
+#endif
   if (b < g.nblocks) {
     p = block_pos(g, b, 3);
     gather3<S, VEC>(v, data, g, p);
   }
+#if ZFP_ALIGNED_PRIO
+  __builtin_amdgcn_s_setprio(0);
+#endif
   {
     const uint4* src = reinterpret_cast<const uint4*>(&kCoderTables);
     uint4* dst = reinterpret_cast<uint4*>(lut);

@@ -1174,6 +1174,15 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
   HIP_TRY(hipGetLastError());
   a.first = 0;
   int passes = 1;
+  // ZFP_HIP_SCAN_TRACE=1: per-pass wall time and moved exits on stderr (diagnostics)
+  const bool trace = getenv("ZFP_HIP_SCAN_TRACE") != nullptr;
+  auto tp = std::chrono::steady_clock::now();
+  if (trace) {
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    fprintf(stderr, "scan: %llu segments of %llu bits, pass 1 %.3f ms\n", (unsigned long long)nseg,
+            (unsigned long long)seg, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count());
+    tp = std::chrono::steady_clock::now();
+  }
   for (;;) {
     uint32_t host_moved = 0;
     HIP_TRY(hipMemcpyAsync(xsnap, xs, nseg * 8, hipMemcpyDeviceToDevice, c->stream));
@@ -1183,6 +1192,12 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
     HIP_TRY(hipMemcpyAsync(&host_moved, moved, 4, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     passes++;
+    if (trace) {
+      const auto t = std::chrono::steady_clock::now();
+      fprintf(stderr, "scan: pass %d %.3f ms, %u exits moved\n", passes,
+              std::chrono::duration<double, std::milli>(t - tp).count(), host_moved);
+      tp = t;
+    }
     if (!host_moved)
       break;
     if ((uint64_t)passes > nseg + 2)

@@ -499,13 +499,7 @@ __global__ __launch_bounds__(256, (kGenWaves<S, REV, HI>)) void encode3_general(
     S v[64];
     BlockPos p = block_pos(g, b, D);
     if constexpr (D == 3 && !kIntField<S>) {
-#if ZFP_GEN_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
       gather3<S, VEC>(v, data, g, p);
-#if ZFP_GEN_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
       return encode_block3<S, REV, false, HI>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
     } else {
       gather_n<S, D>(v, data, g, p);

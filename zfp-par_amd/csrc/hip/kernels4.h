@@ -74,9 +74,6 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   const bool valid = live && b < g.nblocks;
   BlockPos ps{};
   S v[64];
-#if ZFP_GEN_PRIO
-  __builtin_amdgcn_s_setprio(1);
-#endif
   if (valid) {
     const BlockPos p = block_pos(g, b, 4);
     ps = slice_pos(g, p, pad_src_w((int)r, p.cnt[3]));
@@ -86,9 +83,6 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
     for (int i = 0; i < 64; i++)
       v[i] = 0;
   }
-#if ZFP_GEN_PRIO
-  __builtin_amdgcn_s_setprio(0);
-#endif
   __syncthreads();
   uint32_t* d = reinterpret_cast<uint32_t*>(region + (size_t)qd * a.swp);
   Int* X = reinterpret_cast<Int*>(region) + (size_t)(HALF ? (qd & 7u) : qd) * kXStride;

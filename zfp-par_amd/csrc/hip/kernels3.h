@@ -451,8 +451,9 @@ __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* 
                                           uint32_t total);
 
 // Waves per SIMD the general encoder is compiled for: the f64 kernels that code
-// planes 32..63 fit three (<= 168 VGPRs) when their LDS slots are short
-// (launch_encode); the others are not bounded.
+// planes 32..63 fit three (<= 168 VGPRs, 48 bytes of spills) when their LDS
+// slots are short (launch_encode) -- C3 4.44 ms, against 5.44 ms at two waves
+// without spills (profiles/r4u_gw2_ab.txt); the others are not bounded.
 template <typename S, bool REV, bool HI>
 constexpr int kGenWaves = (sizeof(S) == 8 && HI) ? 3 : 1;
 

@@ -207,3 +207,74 @@ def test_block_api_matches_reference(product, ref_capi, d, dt, mode, param):
             want = contig[k] if kind == "contig" else src[sl]
             have = got if kind == "contig" else got[sl]
             assert have.tobytes() == np.ascontiguousarray(want).tobytes()
+
+
+def test_blocks_alloc_beg_matches_reference(prod, ref_capi):
+    """zfp_blocks_alloc_beg (zfp.c:141-147, exported though undeclared): a
+    partition record holding the nchunks + 1 offsets given."""
+    from capi import ZfpBlocks
+    begs = (ctypes.c_size_t * 5)(0, 100, 250, 999, 4096)
+    for api in (prod, ref_capi):
+        fn = _bind(api.lib, "zfp_blocks_alloc_beg", ctypes.POINTER(ZfpBlocks), [sz, vp])
+        b = fn(4, ctypes.cast(begs, vp))
+        assert b.contents.nbeg == 4
+        assert [b.contents.begs[i] for i in range(5)] == list(begs)
+        _bind(api.lib, "zfp_blocks_free", None, [vp])(ctypes.cast(b, vp))
+
+
+def test_compress_call_rejects_a_mismatched_table_entry(prod):
+    """zfp_compress_call / zfp_decompress_call (zfp.h:797-838) with a type or
+    dimensionality that disagrees with the field return 0 and write nothing
+    (no GPU needed to get there)."""
+    lib = prod.lib
+    arr = np.zeros((8, 8, 8), np.float32)
+    field = prod.field_for(arr)
+    zs = lib.zfp_stream_open(None)
+    lib.zfp_stream_set_rate(zs, 8.0, 3, 3, 0)
+    buf = np.zeros(1 << 14, np.uint8)
+    bs = lib.stream_open(buf.ctypes.data, buf.size)
+    lib.zfp_stream_set_bit_stream(zs, bs)
+    ck = lib.zfp_chunk_alloc()
+    lib.zfp_set_chunk_3d(ck, 0, 0, 0, 8, 8, 8)
+    call = _bind(lib, "zfp_compress_call", sz, [vp, vp, vp, u32, u32, u32, u32])
+    dcall = _bind(lib, "zfp_decompress_call", sz, [vp, vp, vp, u32, u32, u32, u32])
+    assert call(zs, ck, field, 0, 0, 2, 3) == 0       # dims 2 for a 3D field
+    assert call(zs, ck, field, 0, 0, 3, 4) == 0       # double for a float field
+    assert call(zs, ck, field, 7, 0, 3, 3) == 0       # no such policy
+    assert dcall(zs, ck, field, 0, 0, 3, 4) == 0
+    assert lib.stream_wtell(bs) == 0 and not buf.any()
+    lib.zfp_chunk_free(ck)
+    lib.stream_close(bs)
+    lib.zfp_stream_close(zs)
+    lib.zfp_field_free(field)
+
+
+@pytest.mark.gpu
+def test_compress_call_matches_compress_chunk(product):
+    """The explicit-policy entry point writes the same stream as
+    zfp_compress_chunk with the stream's own policy."""
+    lib = product.lib
+    rng = np.random.default_rng(3)
+    arr = np.cumsum(rng.standard_normal((12, 20, 24)), axis=2).astype(np.float32)
+    out = []
+    for use_call in (False, True):
+        field = product.field_for(arr)
+        zs = lib.zfp_stream_open(None)
+        lib.zfp_stream_set_precision(zs, 18)
+        buf = np.zeros(1 << 16, np.uint8)
+        bs = lib.stream_open(buf.ctypes.data, buf.size)
+        lib.zfp_stream_set_bit_stream(zs, bs)
+        ck = lib.zfp_chunk_alloc()
+        lib.zfp_set_chunk_3d(ck, 0, 4, 0, 24, 16, 12)
+        if use_call:
+            call = _bind(lib, "zfp_compress_call", sz, [vp, vp, vp, u32, u32, u32, u32])
+            n = call(zs, ck, field, 0, 0, 3, 3)
+        else:
+            n = lib.zfp_compress_chunk(zs, ck, field)
+        assert n > 0
+        out.append(bytes(buf[:n]))
+        lib.zfp_chunk_free(ck)
+        lib.stream_close(bs)
+        lib.zfp_stream_close(zs)
+        lib.zfp_field_free(field)
+    assert out[0] == out[1]

@@ -594,9 +594,9 @@ static uint32_t short_slot_words(const Plan& p)
 // leave (93 words = 5,952 bits); a block that codes longer -- on the C5 field,
 // the blocks that fail the reversible cast test, about 8,300 bits each -- is
 // packed with its first bits and listed, and encode4_patch codes it again with
-// a full slot.  The overflow pool holds every block, so it cannot run out (the
-// round-4 first try sized it for 1/16 of them: more overflowed on C5 and the
-// launch was redone with full slots, 46 -> 90 ms).  C5 chunk 46.4 -> 43.1 ms;
+// a full slot.  The overflow pool holds a quarter of the blocks (the round-4
+// first try sized it for 1/16 of them: more overflowed on C5 and the launch
+// was redone with full slots, 46 -> 90 ms).  C5 chunk 46.4 -> 43.1 ms;
 // 128^4 1.51 -> 1.55 ms (profiles/r4o_4d_slots.txt).  Lossy f32 modes keep
 // full slots (not measured).  ZFP_HIP_SLOT_WORDS=n forces n-word slots (tests
 // of the overflow and patch path), ZFP_HIP_FULL_SLOTS=1 full ones.
@@ -646,7 +646,9 @@ static int run_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out,
     if (!general_args(c, p, nwaves, swp, d_out, g0, index, head.idx_add, a))
       return 0;
     if (swp < swp_full) {
-      uint64_t cap = p.g.nblocks;  // every block may overflow: no redo
+      // a quarter of the blocks (C5: about 1/20 overflow); more makes the
+      // launch redo itself with full slots (correct, slower)
+      uint64_t cap = std::min<uint64_t>(p.g.nblocks, std::max<uint64_t>(65536, p.g.nblocks / 4));
       if (const char* e = getenv("ZFP_HIP_OVF_POOL"))  // tests: force the full-slot redo
         cap = std::max<uint64_t>(1, std::min<uint64_t>(p.g.nblocks, (uint64_t)atoll(e)));
       if (!ensure(c->ovf, cap * sizeof(OvfEntry)))

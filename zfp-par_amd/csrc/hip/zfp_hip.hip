@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <cstdarg>
@@ -600,7 +601,12 @@ static uint32_t short_slot_words(const Plan& p)
 // 128^4 1.51 -> 1.55 ms (profiles/r4o_4d_slots.txt).  Lossy f32 modes keep
 // full slots (not measured).  ZFP_HIP_SLOT_WORDS=n forces n-word slots (tests
 // of the overflow and patch path), ZFP_HIP_FULL_SLOTS=1 full ones.
+// Data whose blocks mostly overflow (noise-like fields) would pay the redo on
+// every call: after a redo the next kFullSlotCalls4 calls of the process take
+// full slots directly, then short slots are tried again.
 constexpr uint32_t kShortSlotWords4 = 93;
+constexpr int kFullSlotCalls4 = 16;
+static std::atomic<int> g_full_slot_calls4{0};
 template <typename S>
 static uint32_t short_slot_words4(const Plan& p)
 {
@@ -608,7 +614,12 @@ static uint32_t short_slot_words4(const Plan& p)
     return ~0u;
   if (const char* e = getenv("ZFP_HIP_SLOT_WORDS"))  // tests: force overflows
     return (uint32_t)atoi(e) | 1u;
-  return p.cp.minexp < kMinExp ? kShortSlotWords4 : ~0u;
+  if (p.cp.minexp >= kMinExp)
+    return ~0u;
+  int n = g_full_slot_calls4.load(std::memory_order_relaxed);
+  while (n > 0 && !g_full_slot_calls4.compare_exchange_weak(n, n - 1, std::memory_order_relaxed)) {
+  }
+  return n > 0 ? ~0u : kShortSlotWords4;
 }
 
 template <typename S>
@@ -664,8 +675,11 @@ static int run_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out,
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
     const int rc = finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
-    if (rc == kRedoFullSlots)
+    if (rc == kRedoFullSlots) {
+      if (!getenv("ZFP_HIP_SLOT_WORDS") && !getenv("ZFP_HIP_OVF_POOL"))
+        g_full_slot_calls4.store(kFullSlotCalls4, std::memory_order_relaxed);
       continue;
+    }
     if (rc != 1 || !a.ovf)
       return rc;
     if constexpr (!kIntField<S>) {

@@ -277,6 +277,13 @@ def _in_buffer(compressed_data):
     return a, a.ctypes.data
 
 
+def _fixed_rate(tolerance, rate):
+    """The mode _set_compression_mode picks is fixed rate (tolerance first, then
+    rate): its stream has no block index, so it is returned as plain bytes and
+    can be written straight into the result object."""
+    return tolerance < 0 and rate >= 0
+
+
 def _check_native(ret, what):
     if ret == 0:
         raise RuntimeError(what)
@@ -361,12 +368,17 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
     field = _make_field(ptr, dtype_to_ztype(dtype), list(reversed(shape)), list(reversed(strides)))
     stream = _lib.zfp_stream_open(None)
     bstream = None
+    target = None
     try:
         if device >= 0:
             _lib.zfp_stream_set_hip_device(stream, device)
         _set_compression_mode(stream, type_none, ndim, tolerance, rate, precision)
         maxsize = _lib.zfp_stream_maximum_size(stream, field)
-        obuf, buf = _out_buffer(maxsize)
+        fixed = _fixed_rate(tolerance, rate)
+        if fixed:
+            target, buf = _bytes_target(maxsize)
+        else:
+            obuf, buf = _out_buffer(maxsize)
         bstream = _lib.stream_open(buf, maxsize)
         _lib.zfp_stream_set_bit_stream(stream, bstream)
         _lib.zfp_stream_rewind(stream)
@@ -375,8 +387,13 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
         n = _lib.zfp_compress(stream, field)
         if n == 0:
             raise RuntimeError("Failed to write to stream")
+        if fixed:
+            out, target = _bytes_take(target, n), None
+            return out
         return _stream_bytes(obuf, n, _export_index(stream))
     finally:
+        if target is not None:
+            _bytes_drop(target)
         _lib.zfp_field_free(field)
         _lib.zfp_stream_close(stream)
         if bstream:
@@ -591,7 +608,8 @@ def _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision,
         _set_compression_mode(stream, type_none, chunkit.ndim, tolerance, rate, precision)
         ck = chunkit.chunk_ptr(ichunk)
         maxsize = _lib.zfp_stream_maximum_size_chunk(stream, field, ck) + (HEADER_MAX_BITS + 63) // 64 * 8 + 8
-        if plain:
+        fixed = _fixed_rate(tolerance, rate)
+        if plain or fixed:
             target, buf = _bytes_target(maxsize)
         else:
             obuf, buf = _out_buffer(maxsize)
@@ -607,6 +625,9 @@ def _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision,
         if plain:
             out, target = _bytes_take(target, n), None
             return out, blob
+        if fixed:  # no block index: the reference's plain bytes
+            out, target = _bytes_take(target, n), None
+            return out
         return _stream_bytes(obuf, n, blob)
     finally:
         if target is not None:

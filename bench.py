@@ -30,8 +30,10 @@ Printed JSON (rank 0): the contract keys plus
   roofline      dominant kernel (c2: encode3_aligned_full) against HBM peak: achieved =
                 algorithmic bytes per launch (4 B read + R/8 B written per value)
                 / mean kernel time from HIP events on the kernel's own stream;
-                traffic = PMC HBM bytes per launch from profiles/<round>_pmc_<workload>.json
-                (rocprofv3 pass, gfx950 FETCH_SIZE x2 correction) or null
+                traffic = PMC HBM bytes per encode call (every dispatch of the call summed)
+                from profiles/<round>_pmc_<workload>.json made by tools/pmc_bench.sh for
+                the same workload and field (gfx950 FETCH_SIZE x2 correction), else null
+                with traffic_null_reason
   cpu_baseline  the reference itself (oracle/_ref/libzfp_ref.so, compiled from
                 /root/reference), OpenMP, every core this process may use, on
                 the full per-GPU field (c2)
@@ -123,20 +125,33 @@ def load_capi(path):
     return ZfpCAPI(path)
 
 
-def traffic_from_profiles(workload, kernel_prefix):
-    """Per-launch HBM bytes of the workload's dominant kernel from the newest committed
-    PMC summary profiles/<round>_pmc_<workload>.json (tools/pmc_summary.py output: a
-    rocprofv3 --pmc pass of this bench command, FETCH_SIZE x2 + WRITE_SIZE), if any."""
-    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_%s.json" % workload)))
+def traffic_from_profiles(workload, field_ext, alg_bytes):
+    """(per-call HBM bytes, source file, reason) of this workload's encode call from the newest
+    committed profiles/<round>_pmc_<workload>.json -- tools/pmc_bench.sh output: rocprofv3 --pmc
+    passes over this bench command, FETCH_SIZE x2 + WRITE_SIZE summed over every dispatch of the
+    call (the main kernel, its fix-ups, a patch or redo launch) and divided by the number of calls.
+    Only a summary made for the same workload, field and algorithmic bytes is taken; otherwise the
+    traffic is null and `reason` says why."""
+    files = sorted(glob.glob(os.path.join(REPO, "profiles", "*pmc_%s.json" % workload)),
+                   key=lambda f: os.path.basename(f).split("_")[0])
+    reason = "no profiles/*pmc_%s.json" % workload
     for f in reversed(files):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        for k, v in d.items():
-            if k.startswith(kernel_prefix) and isinstance(v, dict) and v.get("hbm_bytes_per_launch"):
-                return v["hbm_bytes_per_launch"], os.path.basename(f)
-    return None, None
+        meta, call = d.get("meta") or {}, d.get("encode_call") or {}
+        if meta.get("workload_key") != workload or list(meta.get("field_per_gpu") or []) != list(field_ext):
+            reason = "%s: made for another workload or field" % os.path.basename(f)
+            continue
+        if meta.get("algorithmic_bytes_per_call") != alg_bytes:
+            reason = "%s: algorithmic bytes differ (another stream)" % os.path.basename(f)
+            continue
+        if not call.get("hbm_bytes_per_call"):
+            reason = "%s: no per-call FETCH_SIZE/WRITE_SIZE" % os.path.basename(f)
+            continue
+        return call["hbm_bytes_per_call"], os.path.basename(f), None
+    return None, None, reason
 
 
 def host_cores():
@@ -193,15 +208,14 @@ def cpu_baseline(field_np, mode, param, threads):
 # per workload: BASELINE config, dims, scalar, mode, dominant kernel, CPU-baseline sample (leading slab)
 WORKLOADS = {
     "c2": dict(metric=METRIC, cfg="configs[1]", dtype="f32", mode="rate", param=16,
-               kernel="encode3_aligned_full<float>", sample_planes=None, pmc="encode3_aligned_full<float"),
+               kernel="encode3_aligned_full<float>", sample_planes=None),
     "c3": dict(metric="GB/s uncompressed, 3D float64 fixed-precision-32 encode, device-resident", cfg="configs[2]",
                dtype="f64", mode="precision", param=32, kernel="encode3_general<double, hi planes>",
-               sample_planes=256, pmc="encode3_general<double"),
+               sample_planes=256),
     "c4": dict(metric=METRIC, cfg="configs[3]", dtype="f32", mode="rate", param=8, kernel="encode3_aligned<float>",
-               sample_planes=None, pmc="encode3_aligned<float"),
+               sample_planes=None),
     "c5": dict(metric="GB/s uncompressed, 4D float32 reversible (lossless) encode, device-resident", cfg="configs[4]",
-               dtype="f32", mode="reversible", param=None, kernel="encode4<float, reversible>", sample_planes=4,
-               pmc="encode4<float"),
+               dtype="f32", mode="reversible", param=None, kernel="encode4<float, reversible>", sample_planes=4),
 }
 
 
@@ -324,7 +338,8 @@ def main():
     back_t = torch.empty_like(field_t)
     lib.zfp_field_set_pointer(zf, ctypes.c_void_p(back_t.data_ptr()))
     dms, dkms = [], []
-    for i in range(max(3, args.steps // 2)):
+    n_decode = max(3, args.steps // 2)
+    for i in range(n_decode):
         lib.zfp_stream_rewind(zs)
         if hdr_field is not None:
             lib.stream_rseek(bs, 96)
@@ -383,7 +398,7 @@ def main():
         stream_bytes = nvals * wl["param"] // 8 if wl["mode"] == "rate" else int(nbytes)
         alg_bytes = nvals * es + stream_bytes
         achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-        traffic, tsrc = traffic_from_profiles(args.workload, wl["pmc"])
+        traffic, tsrc, treason = traffic_from_profiles(args.workload, ext, alg_bytes)
         value = world * nvals * es / (ms * 1e-3) / 1e9
         result = {
             "metric": wl["metric"], "value": round(value, 2), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
@@ -394,13 +409,17 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": wl["kernel"], "kernel_ms": round(kernel_ms, 4),
-                         "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": tsrc},
+                         "algorithmic_bytes_per_launch": alg_bytes, "traffic_source": tsrc,
+                         "traffic_per": "encode call (every dispatch of the call summed)",
+                         **({"traffic_null_reason": treason} if traffic is None else {})},
             "call_ms": round(float(np.mean(tms)), 4),
             "decode_ms": round(float(np.mean(dms)), 4) if dms else None,
             "decode_kernel_ms": round(float(np.mean(dkms)), 4) if dkms else None,
             "decode_GBps": round(nvals * es / (np.mean(dms) * 1e-3) / 1e9, 2) if dms else None,
             "gather": gather,
             "clock_warmup": {"ms": args.clock_warm_ms, "launches": warm_launches},
+            "workload_key": args.workload,
+            "calls": {"encode": warm_launches + args.warmup + args.steps, "decode": n_decode},
         }
         result.update(roundtrip)
         if not args.no_cpu and world == 1 and args.workload != "c4":

@@ -42,6 +42,10 @@ inline int __builtin_amdgcn_mov_dpp(int x, int ctrl, int, int, bool)
   g_bar.wait();
   return v;
 }
+inline int __builtin_amdgcn_update_dpp(int, int x, int ctrl, int, int, bool)
+{
+  return __builtin_amdgcn_mov_dpp(x, ctrl, 0, 0, false);
+}
 inline void __syncthreads() { g_bar.wait(); }
 
 #include <cmath>
@@ -118,8 +122,12 @@ static int run(const CodecParams& cp, int type, std::mt19937_64& rng, int trials
       };
       uint32_t* d = reinterpret_cast<uint32_t*>(region.data());
       Int* X = reinterpret_cast<Int*>(xarea.data());
-      len[r] = rev ? encode_block4<S, true>(d, 2 * words - 1, lut, tab, X, region.data(), words, v, cp, reload)
-                   : encode_block4<S, false>(d, 2 * words - 1, lut, tab, X, region.data(), words, v, cp, reload);
+      auto place = [&](bool, uint32_t*& dd, uint32_t& jm) {
+        dd = d;
+        jm = 2 * words - 1;
+      };
+      len[r] = rev ? encode_block4<S, true>(place, lut, tab, X, region.data(), words, v, cp, reload)
+                   : encode_block4<S, false>(place, lut, tab, X, region.data(), words, v, cp, reload);
     });
     bool ok = len[0] == oend && len[1] == len[0] && len[2] == len[0] && len[3] == len[0];
     for (uint32_t i = 0; ok && i < (len[0] + 63) / 64; i++) {

@@ -17,6 +17,14 @@
 inline bool emu_any_all = false;
 static inline int __any(int x) { return x != 0 || emu_any_all; }
 static inline uint64_t __builtin_amdgcn_ballot_w64(bool x) { return (x || emu_any_all) ? 1u : 0u; }
+// llvm.amdgcn.icmp (unsigned): the wave mask of one compare (predicates EQ 32,
+// NE 33, UGT 34, UGE 35, ULT 36, ULE 37), one lane here
+static inline uint64_t __builtin_amdgcn_uicmp(uint32_t a, uint32_t b, int pred)
+{
+  const bool c = pred == 32 ? a == b : pred == 33 ? a != b : pred == 34 ? a > b : pred == 35 ? a >= b
+               : pred == 36 ? a < b : a <= b;
+  return (c || emu_any_all) ? 1u : 0u;
+}
 static inline int __popc(uint32_t x) { return __builtin_popcount(x); }
 static inline int __popcll(uint64_t x) { return __builtin_popcountll(x); }
 static inline int __clzll(long long x) { return x ? __builtin_clzll((uint64_t)x) : 64; }

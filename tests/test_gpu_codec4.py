@@ -145,14 +145,16 @@ def test_short_slots_and_patch_pass_match_oracle_4d(product, oracle, monkeypatch
     _free_index(product)
 
 
-@pytest.mark.parametrize("pack_words", ["1666", "1100", "full"])
+@pytest.mark.parametrize("pack_words", ["1666", "1100", "400", "full"])
 @pytest.mark.parametrize("mode,param", [("precision", 20), ("accuracy", 1e-3), ("reversible", None)])
 def test_packed_staging_decode_matches_oracle_4d(product, oracle, monkeypatch, pack_words, mode, param):
     """Variable-rate decode4 stages each wave's blocks back to back (the
     default, sized for 16 worst-case blocks).  With fewer staged words forced
     (ZFP_HIP_PACK_WORDS), waves whose segment exceeds them (the rough half of
-    the field) make the library repeat the launch with padded slots; "full":
-    padded slots only (ZFP_HIP_FULL_SLOTS)."""
+    the field) make the library repeat the launch with padded slots for them;
+    "full": padded slots only (ZFP_HIP_FULL_SLOTS).  (Decoding such a wave in
+    two passes of eight blocks inside the first launch measured slower -- C5
+    29.4 against 28.6 ms -- as its second decode body spills registers.)"""
     if pack_words == "full":
         monkeypatch.setenv("ZFP_HIP_FULL_SLOTS", "1")
     else:
@@ -166,3 +168,50 @@ def test_packed_staging_decode_matches_oracle_4d(product, oracle, monkeypatch, p
     out, n = product.decompress(want, a.shape, np.float32, mode, param, ztype=TYPE_FLOAT)  # scan-built index
     assert n == len(want)
     assert out.tobytes() == ref_out.tobytes()
+
+
+def _mixed_blocks4(pattern, rng):
+    """A 4D f32 field in whole 4^4 blocks, raster block order (x fastest): block
+    i is random normal data when pattern[i] (it fails the reversible cast: the
+    bits-reinterpreting header, ~8,300 bits) and integer-valued smooth data
+    otherwise (passes the cast, a few thousand bits at most)."""
+    nbx, nby, nbz = 4, 4, 2
+    nbw = -(-len(pattern) // (nbx * nby * nbz))
+    shape = (4 * nbw, 4 * nbz, 4 * nby, 4 * nbx)
+    i = np.indices(shape).astype(np.float32)
+    a = np.round(900 * np.cos(0.07 * i[3] + 0.05 * i[2]) * np.sin(0.03 * i[1] + 0.02 * i[0]))
+    a = a.astype(np.float32)
+    pat = np.zeros(nbw * nbz * nby * nbx, dtype=bool)
+    pat[:len(pattern)] = pattern
+    blk = a.reshape(nbw, 4, nbz, 4, nby, 4, nbx, 4)
+    for b in np.flatnonzero(pat):
+        bx, by, bz, bw = b % nbx, b // nbx % nby, b // (nbx * nby) % nbz, b // (nbx * nby * nbz)
+        blk[bw, :, bz, :, by, :, bx, :] = rng.standard_normal((4, 4, 4, 4))
+    return a
+
+
+@pytest.mark.parametrize("slot_words", [None, "75", "131"])
+def test_big_and_small_slots_4d_reversible(product, oracle, monkeypatch, slot_words):
+    """f32 reversible encode4 with short slots: the blocks of a wave that fail the
+    reversible cast get full slots and the others share the rest of the region
+    (kernels4.h place); waves with more such blocks than fit (here 7, 8, 16 of
+    16 with the default 93-word slots) send the rest to the overflow list and
+    encode4_patch.  Waves of 0, 1, 2, 5, 6, 7, 8 and 16 long blocks, stream and
+    lossless round trip against the oracle; forced slot sizes move the limit."""
+    if slot_words:
+        monkeypatch.setenv("ZFP_HIP_SLOT_WORDS", slot_words)
+    rng = np.random.default_rng(2024)
+    pattern = []
+    for k in (0, 1, 2, 5, 6, 7, 8, 16, 3):
+        wave = np.zeros(16, dtype=bool)
+        wave[rng.choice(16, size=k, replace=False)] = True
+        pattern.extend(wave)
+    a = _mixed_blocks4(pattern, rng)
+    want, _ = _oracle_bytes(oracle, a, "reversible", None)
+    got = product.compress(a, "reversible", None, ztype=TYPE_FLOAT)
+    assert got == want
+    out, n = product.decompress(got, a.shape, np.float32, "reversible", None, ztype=TYPE_FLOAT,
+                                index=product.last_index)
+    assert n == len(got)
+    assert out.tobytes() == a.tobytes()
+    _free_index(product)

@@ -277,3 +277,45 @@ def test_stale_index_with_matching_fingerprint_is_detected(product, oracle, shap
     assert lib.zfp_hip_last_stale_index() == 1
     assert product.last_scan() is not None
     assert got.tobytes() == want.tobytes()
+
+
+GOOD_INDEX_CASES = [(shape, dt, mode, param) for shape in [(8, 12, 8, 20)]
+                    for dt in (np.float32, np.float64, np.int32, np.int64)
+                    for mode, param in (("precision", 20), ("accuracy", 1e-3), ("reversible", None))
+                    if not (np.issubdtype(dt, np.integer) and mode == "accuracy")]
+GOOD_INDEX_CASES += [((1000,), np.float32, "precision", 16), ((40, 52), np.float64, "reversible", None),
+                     ((30, 33, 35), np.float32, "reversible", None)]
+
+
+@pytest.mark.parametrize("shape,dtype,mode,param", GOOD_INDEX_CASES,
+                         ids=["%dD-%s-%s" % (len(c[0]), np.dtype(c[1]).name, c[2]) for c in GOOD_INDEX_CASES])
+def test_encoder_index_is_never_flagged_stale(product, shape, dtype, mode, param):
+    """every decoder checks each block's decoded length against the
+    caller's index (a mismatch means a stale index: rescan, decode again).  An
+    off-by-one in any decoder's `used` would flag every correct index and
+    silently decode twice; so for each block kind -- 4D float/double/int32/int64
+    in the variable-rate modes, and 1D/2D/3D -- the encoder's own index must
+    decode without a scan and without the stale flag, to the same array as the
+    scan-built index."""
+    rng = np.random.default_rng(7)
+    i = np.arange(int(np.prod(shape)), dtype=np.float64).reshape(shape)
+    smooth = np.sin(0.011 * i) + 0.3 * np.cos(0.0007 * i)
+    if np.issubdtype(dtype, np.integer):
+        arr = (smooth * 1e5 + rng.integers(-50, 50, shape)).astype(dtype)
+    else:
+        arr = (smooth + 1e-3 * rng.standard_normal(shape)).astype(dtype)
+    data = product.compress(arr, mode, param)
+    idx = product.last_index
+    assert idx
+    lib = product.lib
+    with_idx, n1 = product.decompress(data, shape, dtype, mode, param, index=idx)
+    assert product.last_scan() is None
+    assert lib.zfp_hip_last_stale_index() == 0
+    lib.zfp_hip_index_free(idx)
+    product.last_index = None
+    no_idx, n2 = product.decompress(data, shape, dtype, mode, param)
+    assert product.last_scan() is not None
+    assert n1 == n2 == len(data)
+    assert with_idx.tobytes() == no_idx.tobytes()
+    if mode == "reversible":
+        assert with_idx.tobytes() == arr.tobytes()

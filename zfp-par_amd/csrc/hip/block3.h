@@ -500,10 +500,7 @@ __device__ __forceinline__ int lossy_emax_cast(int64_t (&q)[64], double (&v)[64]
 // Scheduling fence between the phases of a block (cast, lift, planes, coder):
 // without it the scheduler interleaves neighbouring phases, which keeps both
 // phases' registers live and costs occupancy.
-#ifndef ZFP_PHASE_FENCE
-#define ZFP_PHASE_FENCE 1
-#endif
-#if ZFP_PHASE_FENCE && defined(__HIP_DEVICE_COMPILE__)
+#if defined(__HIP_DEVICE_COMPILE__)
 #define ZFP_PHASE_BARRIER() __builtin_amdgcn_sched_barrier(0)
 #else
 #define ZFP_PHASE_BARRIER() ((void)0)

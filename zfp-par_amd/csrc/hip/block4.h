@@ -29,11 +29,13 @@ namespace zfp_amd {
 // ---------------------------------------------------------------------------
 // quad permutes: DPP quad_perm, lane i of each quad reads lane sel_i
 // (ctrl = sel_0 | sel_1 << 2 | sel_2 << 4 | sel_3 << 6).  Called only where the
-// whole quad is active.
+// whole quad is active.  bound_ctrl (no source lane of a quad_perm is ever
+// invalid, so it changes nothing) lets the compiler fold the permute into the
+// instruction that consumes it (v_max_u32_dpp, v_add_u32_dpp).
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t x)
 {
-  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, CTRL, 0xf, 0xf, false);
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xf, 0xf, true);
 }
 
 template <int CTRL>
@@ -61,16 +63,35 @@ __device__ __forceinline__ U quad_or(U x)
   return x | qperm<kQSwap2>(x);
 }
 
-// exclusive prefix sum over the quad; `total` receives the quad's sum
-__device__ __forceinline__ uint32_t quad_excl(uint32_t x, uint32_t& total)
+// exclusive prefix sum over the quad; `total` receives the quad's sum.  Pair
+// sums s01 (lanes 0,1: x0 + x1; lanes 2,3: x2 + x3), the total from the two
+// pair sums, and lane r's prefix as (odd r: x of lane r-1) + (r >= 2: s01 of
+// lane 0), the lane selections as AND masks: five VALU, each permute folded
+// into its instruction (v_add_u32_dpp, v_and_b32_dpp).
+__device__ __forceinline__ uint32_t quad_excl(uint32_t x, uint32_t& total, uint32_t m_odd, uint32_t m_hi)
+{
+  const uint32_t s01 = x + qperm<0xb1>(x);  // [1,0,3,2]
+  total = s01 + qperm<0x4e>(s01);           // [2,3,0,1]
+  return (qperm<0xa0>(x) & m_odd) + (qperm<0x00>(s01) & m_hi);  // [0,0,2,2], [0,0,0,0]
+}
+
+// the lane masks of quad_excl: m_odd = ~0 on lanes 1 and 3, m_hi = ~0 on lanes
+// 2 and 3 (opaque to the compiler, which would otherwise turn the ANDs into
+// selects and keep the permutes apart)
+__device__ __forceinline__ void quad_excl_masks(uint32_t& m_odd, uint32_t& m_hi)
 {
   const uint32_t r = threadIdx.x & 3u;
-  const uint32_t x1 = qperm<0x90>(x);  // [0,0,1,2]: lane r - 1
-  const uint32_t a = x + (r >= 1u ? x1 : 0u);
-  const uint32_t a2 = qperm<0x40>(a);  // [0,0,0,1]: lane r - 2
-  const uint32_t s = a + (r >= 2u ? a2 : 0u);
-  total = qperm<0xff>(s);  // lane 3
-  return s - x;
+  m_odd = 0u - (r & 1u);
+  m_hi = 0u - (r >> 1);
+  pin_value(m_odd);
+  pin_value(m_hi);
+}
+
+__device__ __forceinline__ uint32_t quad_excl(uint32_t x, uint32_t& total)
+{
+  uint32_t m_odd, m_hi;
+  quad_excl_masks(m_odd, m_hi);
+  return quad_excl(x, total, m_odd, m_hi);
 }
 
 // block max |x| (NaN ignored) over the quad's four slices
@@ -235,25 +256,44 @@ __device__ __forceinline__ void zero_region(uint64_t* w, uint32_t words)
 // 64-bit segments: lane r writes its segment's verbatim bits at pos + 64r and
 // the doubled-ones expansion of its part of xs at the offset given by the
 // quad's exclusive scan of the new ones below it; the lane holding the top
-// one removes the top pair's surplus.  Every slot write is clamped per dword
-// to the slot's last dword (jmax, past the budget), so bits beyond the budget
-// never touch a dword that holds block bits.
-__device__ __forceinline__ void or64_clamped(uint32_t* d, uint32_t jmax, uint32_t p, uint32_t v0, uint32_t v1)
+// one removes the top pair's surplus.
+//
+// Slot writes are funnel-shifted dwords ORed into LDS.  A write of v at bit p
+// covers dwords j-1 .. j+1 (j = ceil(p / 32)); its first dword is clamped to
+// jmax - 2 (one v_min for the three dwords, which then take immediate
+// offsets).  A write clamped that way starts at bit >= 32 (jmax - 1), so it
+// lands in the slot's last three dwords only, which hold no block bits: a slot
+// keeps its first 32 (jmax - 2) bits intact (the host's cap_bits, slot_words4).
+// p >= 1, or p == 0 with a zero first dword (the write at dword -1 ORs 0).
+__device__ __forceinline__ void or64_at(uint32_t* dm, uint32_t jmax, uint32_t p, uint32_t v0, uint32_t v1)
 {
-  const uint32_t j = (p + 31u) >> 5;  // p >= 1: dwords j-1 .. j+1
+  const uint32_t j = min((p + 31u) >> 5, jmax - 1u);
   const uint32_t t = 0u - p;
-  lds_or32(d + min(j - 1u, jmax), __builtin_amdgcn_alignbit(v0, 0u, t));
-  lds_or32(d + min(j, jmax), __builtin_amdgcn_alignbit(v1, v0, t));
-  lds_or32(d + min(j + 1u, jmax), __builtin_amdgcn_alignbit(0u, v1, t));
+  uint32_t* q = dm + j;  // dm = slot - 1 dword: q = dword j - 1
+  lds_or32(q, __builtin_amdgcn_alignbit(v0, 0u, t));
+  lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
+  lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
 }
 
-// v at bit p >= 1: dwords j-1, j, each clamped to jmax
-__device__ __forceinline__ void or32_clamped(uint32_t* d, uint32_t jmax, uint32_t p, uint32_t v)
+// or64_at of a segment write at bit p + 64 r, given jp = ceil(p / 32): the
+// lane's offset of 2 r dwords is folded into its base pointer dmr = dm + 2 r and
+// its clamp jlr = jmax - 1 - 2 r
+__device__ __forceinline__ void or64_seg(uint32_t* dmr, uint32_t jlr, uint32_t jp, uint32_t t, uint32_t v0,
+                                         uint32_t v1)
 {
-  const uint32_t j = (p + 31u) >> 5;
+  uint32_t* q = dmr + min(jp, jlr);
+  lds_or32(q, __builtin_amdgcn_alignbit(v0, 0u, t));
+  lds_or32(q + 1, __builtin_amdgcn_alignbit(v1, v0, t));
+  lds_or32(q + 2, __builtin_amdgcn_alignbit(0u, v1, t));
+}
+
+__device__ __forceinline__ void or32_at(uint32_t* dm, uint32_t jmax, uint32_t p, uint32_t v)
+{
+  const uint32_t j = min((p + 31u) >> 5, jmax - 1u);
   const uint32_t t = 0u - p;
-  lds_or32(d + min(j - 1u, jmax), __builtin_amdgcn_alignbit(v, 0u, t));
-  lds_or32(d + min(j, jmax), __builtin_amdgcn_alignbit(0u, v, t));
+  uint32_t* q = dm + j;
+  lds_or32(q, __builtin_amdgcn_alignbit(v, 0u, t));
+  lds_or32(q + 1, __builtin_amdgcn_alignbit(0u, v, t));
 }
 
 // doubled-ones expansion of 32 bits (32 + popcount bits <= 64)
@@ -263,9 +303,16 @@ __device__ __forceinline__ uint64_t dbl32(const uint32_t* lut, uint32_t x)
   return (uint64_t)dbl16(lut, lo) | ((uint64_t)dbl16(lut, x >> 16) << (16u + (uint32_t)__popc(lo)));
 }
 
-#ifndef ZFP_CODER4_BRANCHY
-#define ZFP_CODER4_BRANCHY 0
-#endif
+// Planes PREC-1 .. kmin of the quad's block from bit `pos` of its slot (d,
+// last dword jmax); returns the end bit, at most lim.  Per plane, with n the
+// coefficients already significant:
+//   nr = clamp(n - 64r, 0, 64)     significant coefficients of the segment
+//   xs = segment >> nr             its not-yet-significant bits
+//   n1 = max(n, quad max of 1 + the top new one)
+//   the plane's length n1 + (new ones) + 1 - [n1 == 256] - [new top one is coefficient 255].
+// Once every active quad of the wave has all 256 coefficients significant, the
+// remaining planes are 256 verbatim bits each (no group tests) and take a short
+// loop of their own (a reversible C5 wave: about 6 of its 30 planes).
 template <int PREC>
 __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, const uint32_t* lut, uint32_t pos,
                                                  uint32_t lim, uint32_t maxprec, const uint32_t (&Pl)[PREC],
@@ -274,92 +321,88 @@ __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, con
   const uint32_t r = threadIdx.x & 3u;
   const uint32_t base = 64u * r;  // first coefficient of this lane's segment
   const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
+  uint32_t* dm = d - 1;
+  uint32_t* dmr = dm + 2u * r;
+  const uint32_t jlr = jmax - 1u - 2u * r;
+  uint32_t m_odd, m_hi;
+  quad_excl_masks(m_odd, m_hi);
   uint32_t p = pos, n = 0;
+  int kf = -1;  // wave-uniform: first plane of the all-significant tail (-1: none)
 #pragma unroll
   for (int k = PREC - 1; k >= 0; k--) {
+    if (kf >= 0)
+      continue;
     const bool act = p < lim && (uint32_t)k >= kmin;  // quad-uniform
-    if (__builtin_amdgcn_ballot_w64(act) == 0)
+    const uint64_t am = lanes_ult(p, lim) & lanes_ule(kmin, (uint32_t)k);  // ballot(act)
+    if (am == 0)
       break;
+    if ((am & lanes_ne(n, 256u)) == 0) {
+      kf = k;
+      continue;
+    }
     const uint64_t P = ((uint64_t)Ph[k] << 32) | Pl[k];
-    const uint32_t nr = n > base ? min(n - base, 64u) : 0u;  // significant coefficients of the segment
-    const uint64_t S = low_mask(nr);
-    const uint64_t N = P & ~S;
-    const uint32_t bl = N ? 64u - (uint32_t)__clzll((long long)N) : 0u;
-    const uint32_t top1 = quad_max(bl ? base + bl : 0u);  // 1 + top new one of the plane (0: none)
-    const uint32_t c = (uint32_t)__popcll(N);
+    const uint32_t nr = (uint32_t)min(max((int)(n - base), 0), 64);  // v_med3_i32
+    // Straight-line for every lane: an inactive lane (or an empty part) ORs
+    // zeros, so no per-lane branch (and no exec-mask bookkeeping) is needed.
+    const uint64_t xs = (act && nr < 64u) ? P >> nr : 0ull;
+    // V = P & low_mask(nv), inactive lanes nv = 0: M = ~0 << nv (0 for nv = 64), V = P & ~M
+    const uint32_t nv = act ? nr : 0u;
+    const uint64_t M = ~0ull << (nv & 63u);
+    const uint32_t Ml = nv < 64u ? (uint32_t)M : 0u, Mh = nv < 64u ? (uint32_t)(M >> 32) : 0u;
+    const uint32_t Vl = __builtin_amdgcn_bitop3_b32(Ml, Pl[k], 0u, 0x0c), Vh = __builtin_amdgcn_bitop3_b32(Mh, Ph[k], 0u, 0x0c);
+    const uint32_t L = xs ? 64u - (uint32_t)__clzll((long long)xs) : 0u;  // xs's length
+    const uint32_t tb = L ? base + nr + L : 0u;                            // 1 + the lane's top new one
+    const uint32_t n1 = quad_max(max(tb, n));
+    const uint32_t c = (uint32_t)__popcll(xs);
     uint32_t ctot;
-    const uint32_t cex = quad_excl(c, ctot);
-    const uint32_t n1 = top1 ? top1 : n;
-    const uint32_t impl = top1 == 256u ? 1u : 0u;  // coefficient 255: its one and test are implicit
-    const uint32_t dlen = n1 + ctot + 1u - (n1 == 256u ? 1u : 0u) - impl;
-#if ZFP_CODER4_BRANCHY
-    if (act) {
-      const uint64_t V = P & S;
-      if (nr)
-        or64_clamped(d, jmax, p + base, (uint32_t)V, (uint32_t)(V >> 32));
-      if (top1 && r == 0u) {  // the plane's positive group test
-        const uint32_t gp = p + n;
-        lds_or32(d + min(gp >> 5, jmax), 1u << (gp & 31u));
-      }
-      const uint64_t xs = nr < 64u ? N >> nr : 0ull;
-      if (xs) {
-        const uint32_t x0 = (uint32_t)xs, x1 = (uint32_t)(xs >> 32);
+    const uint32_t cex = quad_excl(c, ctot, m_odd, m_hi);
+    const bool grow = n1 > n;
+    const uint32_t all = n1 == 256u ? 1u : 0u;
+    const uint32_t impl = grow ? all : 0u;  // coefficient 255: its one and test are implicit
+    const uint32_t dlen = n1 + ctot + 1u - all - impl;
+    or64_seg(dmr, jlr, (p + 31u) >> 5, 0u - p, Vl, Vh);
+    const uint32_t gp = p + n;  // the plane's positive group test
+    lds_or32(d + min(gp >> 5, jmax), (grow && r == 0u) ? 1u << (gp & 31u) : 0u);
+    // Group bits: the expansion of xs unit 0 (bits 0..15) is written here; a
+    // lane whose xs reaches past bit 15 (at most three planes per segment: each
+    // moves the frontier by >= 17) writes its whole expansion again in a
+    // wave-uniform branch (OR is idempotent on the unit-0 bits), as code_planes
+    // does.  The top one at xs bit h: its pair starts at h + (c - 1).
+    const uint32_t x0 = (uint32_t)xs;
+    const bool top = L != 0u && tb == n1;
+    const uint32_t h = L - 1u;
+    const uint32_t t = h + c - 1u;
+    const uint32_t co = p + 1u + base + nr + cex;
+    const uint32_t m0 = (top && h < 16u) ? ((2u | impl) << (t & 31u)) : 0u;
+    or32_at(dm, jmax, co, dbl16(lut, x0 & 0xffffu) & ~m0);
+    const bool ext = (xs >> 16) != 0ull;
+    if ((lanes_ne((uint32_t)(xs >> 32), 0u) | lanes_ugt((uint32_t)xs, 0xffffu)) != 0) {
+      if (ext) {
+        const uint32_t x1 = (uint32_t)(xs >> 32);
         uint64_t E0 = dbl32(lut, x0), E1 = dbl32(lut, x1);
         const uint32_t L0 = 32u + (uint32_t)__popc(x0);
-        if (base + bl == top1) {
-          // top one at xs bit h; its pair starts at h + (c - 1) of the expansion
-          const uint32_t h = bl - 1u - nr;
-          const uint32_t t = h + c - 1u;
-          if (h < 32u)
-            E0 &= ~((uint64_t)(2u | impl) << t);
-          else
-            E1 &= ~((uint64_t)(2u | impl) << (t - L0));
-        }
-        const uint32_t co = p + 1u + base + nr + cex;
-        or64_clamped(d, jmax, co, (uint32_t)E0, (uint32_t)(E0 >> 32));
-        if (x1)
-          or64_clamped(d, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
+        const uint64_t m = top ? (uint64_t)(2u | impl) : 0ull;
+        E0 &= ~(h < 32u ? m << (t & 63u) : 0ull);
+        E1 &= ~(h < 32u ? 0ull : m << ((t - L0) & 63u));
+        or64_at(dm, jmax, co, (uint32_t)E0, (uint32_t)(E0 >> 32));
+        or64_at(dm, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
       }
     }
-#else
-    // Straight-line for every lane: an inactive lane (or an empty part) ORs
-    // zeros at a clamped address, so no per-lane branch (and no exec-mask
-    // bookkeeping in SGPRs) is needed.  Group bits: the expansion of the
-    // segment's xs unit 0 (bits 0..15) is written here; a lane whose xs
-    // reaches past bit 15 (at most three planes per segment: each moves the
-    // frontier by >= 17) writes its whole expansion again in a wave-uniform
-    // branch (OR is idempotent on the unit-0 bits), as code_planes does.
-    {
-      const uint64_t V = act ? P & S : 0ull;
-      or64_clamped(d, jmax, p + base, (uint32_t)V, (uint32_t)(V >> 32));
-      const uint32_t gp = p + n;  // the plane's positive group test
-      lds_or32(d + min(gp >> 5, jmax), (act && top1 && r == 0u) ? 1u << (gp & 31u) : 0u);
-      const uint64_t xs = (act && nr < 64u) ? N >> nr : 0ull;
-      const uint32_t x0 = (uint32_t)xs;
-      // top one at xs bit h; its pair starts at h + (c - 1) of the expansion
-      const bool top = bl != 0u && base + bl == top1;
-      const uint32_t h = bl - 1u - nr;
-      const uint32_t t = h + c - 1u;
-      const uint32_t co = p + 1u + base + nr + cex;
-      const uint32_t m0 = (top && h < 16u) ? ((2u | impl) << (t & 31u)) : 0u;
-      or32_clamped(d, jmax, co, dbl16(lut, x0 & 0xffffu) & ~m0);
-      const bool ext = (xs >> 16) != 0ull;
-      if (__builtin_amdgcn_ballot_w64(ext) != 0) {
-        if (ext) {
-          const uint32_t x1 = (uint32_t)(xs >> 32);
-          uint64_t E0 = dbl32(lut, x0), E1 = dbl32(lut, x1);
-          const uint32_t L0 = 32u + (uint32_t)__popc(x0);
-          const uint64_t m = top ? (uint64_t)(2u | impl) : 0ull;
-          E0 &= ~(h < 32u ? m << (t & 63u) : 0ull);
-          E1 &= ~(h < 32u ? 0ull : m << ((t - L0) & 63u));
-          or64_clamped(d, jmax, co, (uint32_t)E0, (uint32_t)(E0 >> 32));
-          or64_clamped(d, jmax, co + L0, (uint32_t)E1, (uint32_t)(E1 >> 32));
-        }
-      }
-    }
-#endif
     p = act ? p + dlen : p;
     n = act ? n1 : n;
+  }
+  if (kf >= 0) {
+    // every active quad has n == 256: a plane is its 256 bits verbatim
+#pragma unroll
+    for (int k = PREC - 1; k >= 0; k--) {
+      if (k > kf)
+        continue;
+      const bool act = p < lim && (uint32_t)k >= kmin;
+      if ((lanes_ult(p, lim) & lanes_ule(kmin, (uint32_t)k)) == 0)
+        break;
+      or64_seg(dmr, jlr, (p + 31u) >> 5, 0u - p, act ? Pl[k] : 0u, act ? Ph[k] : 0u);
+      p = act ? p + 256u : p;
+    }
   }
   return p < lim ? p : lim;
 }
@@ -476,12 +519,16 @@ __device__ __forceinline__ int lossy_emax_cast4(int64_t (&q)[64], double (&v)[64
   return emax;
 }
 
-// Encode the quad's block into its zeroed slot (d: dwords, jmax: last dword);
-// returns the block length in bits including minbits padding.  Called by the
-// whole wave: the exchange and the slot zeroing are wave-wide (`region`,
-// `region_words`: the wave's slot area, which aliases the exchange areas).
-template <typename S, bool REV, bool HALF = false, typename Reload>
-__device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, const uint32_t* lut, const uint32_t* tab,
+// Encode the quad's block into its zeroed slot; returns the block length in
+// bits including minbits padding.  Called by the whole wave: the exchange and
+// the slot zeroing are wave-wide (`region`, `region_words`: the wave's slot
+// area, which aliases the exchange areas).  The slot comes from
+// place(big, d, jmax), called by the whole wave once the region is zeroed
+// (d: the slot's dwords, jmax: its last dword); big: the block codes with the
+// reversible reinterpreted-bits header (the long ones, about 8,300 bits on
+// f32 data), so a kernel with short slots can give it a full one.
+template <typename S, bool REV, bool HALF = false, typename Place, typename Reload>
+__device__ __forceinline__ uint32_t encode_block4(Place&& place, const uint32_t* lut, const uint32_t* tab,
                                                   typename Traits<S>::Int* X, uint64_t* region, uint32_t region_words,
                                                   S (&v)[64], const CodecParams& cp, Reload&& reload)
 {
@@ -491,7 +538,8 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
   constexpr uint32_t kE = T::kEbits;
   constexpr int PREC = T::kIntPrec;
   const uint32_t r = threadIdx.x & 3u;
-  OrSlot os{reinterpret_cast<uint64_t*>(d), jmax};
+  uint32_t* d;
+  uint32_t jmax;
   Int q[64];
   uint32_t Pl[PREC], Ph[PREC];
   if constexpr (std::is_integral<S>::value) {
@@ -503,6 +551,8 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
     xform<3, false, REV>(q);
     exchange_fwd<REV, HALF>(q, X, tab);
     zero_region(region, region_words);
+    place(false, d, jmax);
+    OrSlot os{reinterpret_cast<uint64_t*>(d), jmax};
     uint32_t prec = cp.maxprec, bits = 0;
     if constexpr (REV) {
       UInt all = 0;
@@ -527,12 +577,45 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
     return end < cp.minbits ? cp.minbits : end;
   } else if constexpr (REV) {
     // reversible (revencodef.c:45-80)
-    const int emax = block_emax(quad_absmax(v));
+    int emax;
+    bool fast = false;  // wave-uniform: no inf/NaN in any block of the wave (f32)
+    if constexpr (sizeof(S) == 4) {
+      // block maximum from integer maxima of the bit patterns (as
+      // lossy_emax_cast4): a tree of v_max3 instead of a chain of 64 float
+      // compares; NaN sorts above inf, so one compare flags the blocks that
+      // need the exact NaN-ignoring maximum
+      int32_t mi = 0;
+      uint32_t mu = 0;
+#pragma unroll
+      for (int i = 0; i < 64; i++) {
+        const uint32_t b = __float_as_uint(v[i]);
+        mi = max(mi, (int32_t)b);
+        mu = max(mu, b);
+      }
+      const uint32_t mb = quad_max(max((uint32_t)mi, mu & 0x7fffffffu));
+      fast = !__any(mb >= 0x7f800000u);
+      emax = mb == 0 ? -127 : ((mb >> 23) == 0 ? -126 : (int)(mb >> 23) - 126);
+    }
+    if (!fast)
+      emax = block_emax(quad_absmax(v));
     // bitwise accumulation: a short-circuit && becomes 64 nested lane branches
     decltype(bits_of(v[0])) sdiff = 0;
     bool same;
     if (emax != -T::kEbias) {
-      fwd_cast(q, v, emax);
+      if constexpr (sizeof(S) == 4) {
+        if (fast) {
+          // finite block: |2^(30 - emax) x| < 2^30, the plain conversion is the
+          // reference's (no x86 out-of-range emulation needed)
+          const float sc = pow2f(30 - emax);
+#pragma unroll
+          for (int i = 0; i < 64; i++)
+            q[i] = (int32_t)(sc * v[i]);
+        } else {
+          fwd_cast(q, v, emax);
+        }
+      } else {
+        fwd_cast(q, v, emax);
+      }
       const S s = (sizeof(S) == 4) ? (S)pow2f(emax - 30) : (S)pow2d(emax - 62);
 #pragma unroll
       for (int i = 0; i < 64; i++) {
@@ -560,6 +643,8 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
     xform<3, false, true>(q);
     exchange_fwd<true, HALF>(q, X, tab);
     zero_region(region, region_words);
+    place(!same, d, jmax);
+    OrSlot os{reinterpret_cast<uint64_t*>(d), jmax};
     const uint32_t e = (uint32_t)(emax + T::kEbias);
     if (same && !e)
       return 1u < cp.minbits ? cp.minbits : 1u;  // a single 0 bit
@@ -602,6 +687,8 @@ __device__ __forceinline__ uint32_t encode_block4(uint32_t* d, uint32_t jmax, co
     xform<3, false, false>(q);
     exchange_fwd<false, HALF>(q, X, tab);
     zero_region(region, region_words);
+    place(false, d, jmax);
+    OrSlot os{reinterpret_cast<uint64_t*>(d), jmax};
     uint32_t bits = 1;
     if (e) {
       if (r == 0u) os.head(2 * e + 1);

@@ -298,32 +298,31 @@ __device__ __forceinline__ void pin_registers(U (&a)[N])
 // per-block index check included); the f32 decoder's instruction-cache misses
 // 5.8 -> 3.7 per wave at the same time (profiles/r4m_cold_ab.txt)
 #define ZFP_RARE(x) __builtin_expect(!!(x), 0)
+
+// Wave masks of a 32-bit unsigned compare (one v_cmp into an SGPR pair), for
+// wave-level decisions: the same bits as __builtin_amdgcn_ballot_w64(a OP b),
+// which the compiler tends to lower as a select, a compare and the ballot when
+// the condition is combined with others.
+__device__ __forceinline__ uint64_t lanes_ult(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 36); }
+__device__ __forceinline__ uint64_t lanes_ule(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 37); }
+__device__ __forceinline__ uint64_t lanes_ugt(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 34); }
+__device__ __forceinline__ uint64_t lanes_ne(uint32_t a, uint32_t b) { return __builtin_amdgcn_uicmp(a, b, 33); }
 // Bit reader over a word array in LDS (or global memory).
 struct WordReader {
   const uint64_t* w;
   uint32_t pos;  // bit position within the lane's slot (slots are small)
 
-#ifndef ZFP_PEEK_DWORDS
-#define ZFP_PEEK_DWORDS 1
-#endif
-  // Branch-free 64-bit window at bit p.  Dword form: the three dwords from
-  // dword p/32 on, funnel-shifted by p % 32 (two v_alignbit_b32; a 64-bit
-  // shift costs about three times a 32-bit op); they stay inside the slot,
-  // which has a spare word past its last.  Word form: both words are always
-  // read, and (b << 1) << (63 - s) vanishes at s = 0.
+  // Branch-free 64-bit window at bit p: the three dwords from dword p/32 on,
+  // funnel-shifted by p % 32 (two v_alignbit_b32; a 64-bit shift costs about
+  // three times a 32-bit op); they stay inside the slot, which has a spare
+  // word past its last.
   __device__ __forceinline__ uint64_t peek_at(uint32_t p) const
   {
-#if ZFP_PEEK_DWORDS
     const uint32_t* d = reinterpret_cast<const uint32_t*>(w) + (p >> 5);
     const uint32_t s = p & 31u;
     const uint32_t d0 = d[0], d1 = d[1], d2 = d[2];
     const uint32_t lo = __builtin_amdgcn_alignbit(d1, d0, s), hi = __builtin_amdgcn_alignbit(d2, d1, s);
     return ((uint64_t)hi << 32) | lo;
-#else
-    const uint32_t i = p >> 6, s = p & 63u;
-    const uint64_t a = w[i], b = w[i + 1];
-    return (a >> s) | ((b << 1) << (63u - s));
-#endif
   }
   __device__ __forceinline__ uint64_t peek64() const { return peek_at(pos); }
   __device__ __forceinline__ uint64_t read(uint32_t n)
@@ -1059,15 +1058,8 @@ __device__ __forceinline__ uint32_t squeeze32(const uint32_t* sq, uint32_t f)
 // section is parsed in closed form and its consumption selected); only lanes
 // whose section is not closed-form run the reference loop, in a wave-uniform
 // branch.
-// ZFP_DP64_NOINLINE (experiment): one out-of-line copy instead of one per
-// unrolled plane, against the decoder's instruction-cache misses
-#if ZFP_DP64_NOINLINE
-#define ZFP_DP64_ATTR __attribute__((noinline))
-#else
-#define ZFP_DP64_ATTR __forceinline__
-#endif
 template <bool IMP = true, int SIZE = 64>
-__device__ ZFP_DP64_ATTR uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
+__device__ __forceinline__ uint64_t decode_plane64(WordReader& r, const uint32_t* sq, uint32_t& bits, uint32_t& n)
 {
   const uint32_t m = n < bits ? n : bits;
   uint32_t pos = r.pos;
@@ -1178,15 +1170,8 @@ __device__ __forceinline__ uint32_t decode_planes64(WordReader& r, const uint32_
 // its budget could end inside the plane (bits < 64); past its precision limit
 // a lane reads nothing.  Once some lane has 32 significant coefficients the
 // remaining planes go to decode_plane64 for every lane.
-#ifndef ZFP_DEC32
-#define ZFP_DEC32 1
-#endif
-// ZFP_DEC32_SWITCH (experiment): leave the 32-bit body at the first plane with
-// a slow lane instead of running decode_plane64 for that lane inline
-#ifndef ZFP_DEC32_SWITCH
-#define ZFP_DEC32_SWITCH 0
-#endif
-// more lanes than this in a plane's slow path: the rest of the block without the 32-bit body
+// more lanes than this in a plane's slow path: the rest of the block without the
+// 32-bit body (tests/test_emu.py sets it to 0 to run the switch on every slow plane)
 #ifndef ZFP_DEC32_DENSE
 #define ZFP_DEC32_DENSE 16
 #endif
@@ -1194,9 +1179,6 @@ template <bool IMP = true>
 __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_t* sq, uint32_t budget,
                                                     uint32_t maxprec, uint64_t (&P)[32])
 {
-#if !ZFP_DEC32
-  return decode_planes64<32, IMP>(r, sq, budget, maxprec, P);
-#else
   const uint32_t kmin = 32u > maxprec ? 32u - maxprec : 0u;
   uint32_t bits = budget, n = 0;
 #pragma unroll
@@ -1236,22 +1218,12 @@ __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_
     const uint32_t xx = squeeze32(sq, F);
     const uint32_t x = ubfe(lo, 0u, n) | (xx << n);
     const uint32_t used = n + (one ? q + 2u : 1u);
-#if ZFP_DEC32_SWITCH
-    // no decode_plane64 inside this loop (half the decoder's code): the first
-    // plane some lane cannot take here goes, with the rest, to the loop below
-    if (__builtin_amdgcn_ballot_w64(act && !fast) != 0) {
-      m32 = false;
-      ksw = k;
-      continue;
-    }
-#endif
     if (fast) {
       P[k] = x;
       r.pos += used;
       bits -= used;
       n += one ? np : 0u;
     }
-#if !ZFP_DEC32_SWITCH
     const bool slow = act && !fast;
     const uint64_t sm = __builtin_amdgcn_ballot_w64(slow);
     if (ZFP_RARE(sm != 0)) {
@@ -1267,7 +1239,6 @@ __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_
         ksw = k - 1;
       }
     }
-#endif
   }
   if (!m32) {
 #pragma unroll
@@ -1283,7 +1254,6 @@ __device__ __forceinline__ uint32_t decode_planes32(WordReader& r, const uint32_
     }
   }
   return budget - bits;
-#endif
 }
 
 }  // namespace zfp_amd

@@ -322,6 +322,9 @@ struct GeneralArgs {
   uint32_t ovf_cap;       // pool slots
   uint32_t ovf_swp;       // words per pool slot
   uint32_t cap_bits;      // intact bits of an LDS slot
+#ifdef ZFP_EXP4_TRACE
+  uint64_t* trace;        // experiment: per-phase clocks of every 64th wave (encode4)
+#endif
 };
 
 // Overflow slot of a lane whose block did not fit its LDS slot: ~0u when none
@@ -405,16 +408,20 @@ __device__ __forceinline__ uint64_t wave_sum64(uint64_t x)
 // a one-lane walk pays one round trip per predecessor, holding the wave's slots
 // meanwhile; the window makes that chain 64 times shorter.  Called by every
 // lane of the wave with the same arguments.
-__device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
+// First half of lookback_wave: publish the wave's aggregate (wave 0: its
+// inclusive prefix), so successors can look past it while it does other work.
+__device__ __forceinline__ void lookback_publish(uint64_t* status, uint64_t w, uint32_t agg)
+{
+  if ((threadIdx.x & 63u) == 0)
+    __hip_atomic_store(&status[w], (w == 0 ? kStIncl : kStAgg) | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Second half: walk back to an inclusive prefix, publish the wave's own.
+__device__ __forceinline__ uint64_t lookback_walk(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
 {
   const uint32_t lane = threadIdx.x & 63u;
-  if (w == 0) {
-    if (lane == 0)
-      __hip_atomic_store(&status[0], kStIncl | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (w == 0)
     return 0;
-  }
-  if (lane == 0)
-    __hip_atomic_store(&status[w], kStAgg | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint64_t excl = 0;
   int64_t top = (int64_t)w - 1;
   uint32_t spins = 0;
@@ -445,10 +452,16 @@ __device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint64_t w, 
   return excl;
 }
 
-template <int NB, bool OVF>
+__device__ __forceinline__ uint64_t lookback_wave(uint64_t* status, uint64_t w, uint32_t agg, uint32_t* error)
+{
+  lookback_publish(status, w, agg);
+  return lookback_walk(status, w, agg, error);
+}
+
+template <int NB, bool OVF, typename SlotOf>
 __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
                                           const uint32_t* wrt, const uint32_t* ovi, uint64_t w, uint64_t start,
-                                          uint32_t total);
+                                          uint32_t total, SlotOf&& slot_of);
 
 // Waves per SIMD the general encoder is compiled for: the f64 kernels that code
 // planes 32..63 fit three (<= 168 VGPRs, 48 bytes of spills) when their LDS
@@ -568,9 +581,11 @@ __global__ __launch_bounds__(256, (kGenWaves<S, REV, HI>)) void encode3_general(
   __builtin_amdgcn_wave_barrier();
   if (spill) {
     __threadfence();  // the overflow slots' atomics have landed before they are read
-    pack_wave<64, true>(a, wbase, off, wrt, ovi, w, start, total);
+    pack_wave<64, true>(a, wbase, off, wrt, ovi, w, start, total,
+                        [&](uint32_t l) { return wbase + (size_t)l * a.swp; });
   } else {
-    pack_wave<64, false>(a, wbase, off, wrt, ovi, w, start, total);
+    pack_wave<64, false>(a, wbase, off, wrt, ovi, w, start, total,
+                         [&](uint32_t l) { return wbase + (size_t)l * a.swp; });
   }
 }
 
@@ -580,10 +595,11 @@ __global__ __launch_bounds__(256, (kGenWaves<S, REV, HI>)) void encode3_general(
 // (shared with the neighbouring waves) go to the partials for the fix-up
 // kernels.  Shared by encode3_general (NB = 64) and encode4 (NB = 16).
 // OVF: some blocks of the wave sit in overflow slots (ovi[l] != kNoSlot).
-template <int NB, bool OVF>
+// slot_of(l): the first word of block l's slot.
+template <int NB, bool OVF, typename SlotOf>
 __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* wbase, const uint32_t* off,
                                           const uint32_t* wrt, const uint32_t* ovi, uint64_t w, uint64_t start,
-                                          uint32_t total)
+                                          uint32_t total, SlotOf&& slot_of)
 {
   const int lane = threadIdx.x & 63;
   const uint64_t G = a.g0 + start;
@@ -620,7 +636,7 @@ __device__ __forceinline__ void pack_wave(const GeneralArgs& a, const uint64_t* 
         if (OVF && ovi[l] != kNoSlot)
           bits = slot_bits_l2(a.ovf + (size_t)ovi[l] * a.ovf_swp, sp, cnt);
         else
-          bits = slot_bits(wbase + (size_t)l * a.swp, sp, cnt);
+          bits = slot_bits(slot_of((uint32_t)l), sp, cnt);
         val |= bits << (x0 - lo);
       }
     }

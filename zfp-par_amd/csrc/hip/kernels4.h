@@ -18,15 +18,27 @@ namespace zfp_amd {
 
 constexpr uint32_t kBlocks4PerWave = 16;
 // LDS words ahead of the slot / exchange region.  Encoder: doubled-ones table
-// (256 dwords), order table (64), per-block offsets and written counts (16+16).
+// (256 dwords), order table (64), per-block bit offsets and written counts
+// (16 + 16).  (f32 reversible: 176 + 16 x 93 words = 13,312 bytes, 12 waves
+// per CU at the 512-byte LDS granule; 8 more bytes would cost a wave.)
 constexpr uint32_t kEnc4HeadWords = (256 + 64 + 16 + 16) / 2;
+// Short reversible slots (a.ovf set): a block that fails the reversible cast
+// (the reinterpreted-bits header, about 8,300 bits on f32 data -- 7.5 % of the
+// C5 blocks, in half of its waves) gets a full slot of a.ovf_swp words, the
+// others share the rest of the wave's 16 a.swp words, at least kMinSlot4
+// words each (4,192 bits: 99.9 % of the other C5 blocks code shorter).
+// Blocks that still outrun their slot (a long cast block, more big blocks
+// than fit) take the overflow list and encode4_patch.
+constexpr uint32_t kMinSlot4 = 67;
 // Decoder: order table (64 dwords), per-block stream bit offsets (16).
 constexpr uint32_t kDec4HeadWords = (64 + 16) / 2;
 
-// Slot of a 4D block with budget `lim` bits: its dwords plus two spare dwords
-// (targets of the clamped writes past the budget); odd, so the 16 slots of a
-// wave start on different banks.
-__host__ __device__ constexpr uint32_t slot_words4(uint32_t lim) { return ((((lim + 31u) >> 5) + 3u) / 2u) | 1u; }
+// Slot of a 4D block with budget `lim` bits: its dwords plus three spare
+// dwords (targets of the clamped writes past the budget, block4.h or64_at);
+// odd, so the 16 slots of a wave start on different banks.
+__host__ __device__ constexpr uint32_t slot_words4(uint32_t lim) { return ((((lim + 31u) >> 5) + 4u) / 2u) | 1u; }
+// Bits of a slot of swp words that clamped writes never touch
+__host__ __device__ constexpr uint32_t slot_cap_bits4(uint32_t swp) { return 32u * (2u * swp - 3u); }
 
 // Overflow list of the short-slot 4D encoder: a block longer than its LDS slot
 // is packed with its first cap_bits only (the rest zero) and listed with its
@@ -36,6 +48,92 @@ struct OvfEntry {
   uint64_t b;    // block
   uint64_t pos;  // bit position of its first bit relative to out[0]
 };
+
+// In-place compaction of a wave's 16 slots into one bit string in LDS (local
+// bit 0 = the wave's first block), before its stream offset is known: block q
+// (wrt[q] bits at bit 0 of slot_of(q)) moves to local bit off[q], one block
+// after another.  Safe in place when every block fits its slot (the caller's
+// `simple` test): block q's destination ends at off[q + 1] <= 64 x the words
+// of slots 0..q, i.e. before slot q + 1, and within a block every lane reads
+// its words before any lane writes.  A block's first word ORs onto the end of
+// the previous block; every other word is stored whole (zero past the block).
+// NT: words per lane of the longest slot (f32: 136 words, f64: 263).
+template <int NT, typename SlotOf>
+__device__ __forceinline__ void compact_wave4(uint64_t* region, const uint32_t* off, const uint32_t* wrt,
+                                              SlotOf&& slot_of)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t q = 0; q < kBlocks4PerWave; q++) {
+    const uint32_t L = wrt[q], D = off[q];
+    const uint64_t* src = slot_of(q);
+    const uint32_t d0 = D & 63u, nwq = (d0 + L + 63u) >> 6;
+    uint64_t v[NT];
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      const uint32_t k = lane + 64u * t;
+      const int64_t lo = (int64_t)k * 64 - d0;  // block bit at the word's bit 0
+      const int64_t x0 = lo > 0 ? lo : 0, x1 = lo + 64 < (int64_t)L ? lo + 64 : (int64_t)L;
+      v[t] = (k < nwq && x0 < x1) ? slot_bits(src, (uint32_t)x0, (uint32_t)(x1 - x0)) << (x0 - lo) : 0ull;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the block's reads have returned
+    __builtin_amdgcn_wave_barrier();
+    uint64_t* dst = region + (D >> 6);
+#pragma unroll
+    for (int t = 0; t < NT; t++) {
+      const uint32_t k = lane + 64u * t;
+      if (k < nwq) {
+        if (k == 0 && d0)
+          dst[0] |= v[t];
+        else
+          dst[k] = v[t];
+      }
+    }
+    // LDS operations of a wave complete in order: the next block reads after these writes
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
+// Copy-out of a compacted wave (local words loc[0 ..]) to its stream bits
+// [G, G + total), G = g0 + start: every output word is a funnel shift of two
+// local words; the first and last word (shared with the neighbouring waves) go
+// to the partials for the fix-up kernels, as in pack_wave.
+__device__ __forceinline__ void copy_out_wave(const GeneralArgs& a, const uint64_t* loc, uint64_t w, uint64_t start,
+                                              uint32_t total)
+{
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t G = a.g0 + start;
+  const uint64_t W0 = G >> 6;
+  const uint32_t r0 = (uint32_t)(G & 63);
+  const uint64_t end = G + total;
+  const uint32_t nw = (uint32_t)(((end - 1) >> 6) - W0 + 1);
+  const uint32_t nloc = (total + 63u) >> 6;
+  const bool head_part = r0 != 0 || (nw == 1 && (end & 63));
+  const bool tail_part = (end & 63) != 0;
+  for (uint32_t o = lane; o < nw; o += 64) {
+    const uint64_t cur = o < nloc ? loc[o] : 0ull;
+    const uint64_t prev = (o >= 1 && o - 1 < nloc) ? loc[o - 1] : 0ull;
+    const uint64_t val = r0 ? (cur << r0) | (prev >> (64 - r0)) : cur;
+    const bool head = o == 0 && head_part;
+    const bool tail = o == nw - 1 && tail_part;
+    if (head || tail)
+      a.partials[2 * w + (o == 0 ? 0 : 1)] = Partial{W0 + o, val};
+    else
+      a.out[W0 + o] = val;
+  }
+  if (lane == 0) {
+    if (!head_part)
+      a.partials[2 * w].idx = kNoWord;
+    if (!tail_part || nw == 1)
+      a.partials[2 * w + 1].idx = kNoWord;
+  }
+}
+
+// bits of a block to copy from its slot: all of them, or the intact cap of an
+// overflowed block, or the slot (past it a block holds minbits padding zeros)
+__device__ __forceinline__ uint32_t wrt_of(uint32_t len, uint32_t sw, uint32_t cap, bool over)
+{
+  return over ? cap : (len < 64 * sw ? len : 64 * sw);
+}
 
 // HALF: exchange areas shared by quads q and q + 8 (block4.h exchange_fwd), so
 // the LDS region is max(16 slots, 8 exchange areas); with a.ovf the slots are
@@ -57,6 +155,12 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   reinterpret_cast<uint4*>(lut)[lane] = reinterpret_cast<const uint4*>(kCoderTables.dbl)[lane];
   tab[lane] = kOrderTab4.t[lane];
 
+#ifdef ZFP_EXP4_TRACE
+  const uint64_t tr0 = wall_clock64();
+#define ZFP_TR4(i) do { if (a.trace && (w & 63) == 0 && lane == 0) a.trace[(w >> 6) * 8 + (i)] = wall_clock64() - tr0; } while (0)
+#else
+#define ZFP_TR4(i) ((void)0)
+#endif
   const uint64_t nwaves = (g.nblocks + kBlocks4PerWave - 1) / kBlocks4PerWave;
   uint64_t w;
   if (a.var) {
@@ -67,6 +171,7 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   } else {
     w = blockIdx.x;
   }
+  ZFP_TR4(0);
   const bool live = w < nwaves;
   const uint64_t first = w * kBlocks4PerWave;
   const uint32_t qd = lane >> 2, r = lane & 3u;
@@ -84,9 +189,42 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
       v[i] = 0;
   }
   __syncthreads();
-  uint32_t* d = reinterpret_cast<uint32_t*>(region + (size_t)qd * a.swp);
+#ifdef ZFP_EXP4_TRACE
+  __builtin_amdgcn_s_waitcnt(0x0f70);  // vmcnt(0): the gather has landed
+  ZFP_TR4(1);
+#endif
   Int* X = reinterpret_cast<Int*>(region) + (size_t)(HALF ? (qd & 7u) : qd) * kXStride;
-  uint32_t len = encode_block4<S, REV, HALF>(d, 2 * a.swp - 1, lut, tab, X, region, kBlocks4PerWave * a.swp, v, cp,
+  // Slot layout of the wave's region (wave-uniform): block l's slot starts at
+  // word gb * B + (l - gb) * small, gb = min(big blocks below l, m), and the
+  // first m big blocks have B words; uniform a.swp words unless short
+  // reversible slots meet a big block.
+  uint64_t bm = 0;                         // bit 4l: block l is big
+  uint32_t m = 0, small = a.swp, B = a.swp;
+  auto slot_words_of = [&](uint32_t l) -> uint32_t {
+    const uint32_t below = (uint32_t)__popcll(bm & ((1ull << (4u * l)) - 1ull));
+    const uint32_t gb = min(below, m);
+    return gb * B + (l - gb) * small;
+  };
+  uint32_t sw = a.swp;  // the quad's slot words
+  auto place = [&](bool big, uint32_t*& d, uint32_t& jmax) {
+    ZFP_TR4(2);
+    if (REV && a.ovf) {
+      bm = __builtin_amdgcn_ballot_w64(big && r == 0u) & 0x1111111111111111ull;
+      if (bm) {
+        const uint32_t R = kBlocks4PerWave * a.swp;
+        B = a.ovf_swp;
+        // big slots granted: as many as leave kMinSlot4 words for every other block
+        const uint32_t fit = R > kBlocks4PerWave * kMinSlot4 ? (R - kBlocks4PerWave * kMinSlot4) / (B - kMinSlot4) : 0u;
+        m = min((uint32_t)__popcll(bm), fit);  // < 16: R < 16 B
+        small = (((R - m * B) / (kBlocks4PerWave - m)) - 1u) | 1u;  // odd
+        const uint32_t below = (uint32_t)__popcll(bm & ((1ull << (4u * qd)) - 1ull));
+        sw = (big && below < m) ? B : small;
+      }
+    }
+    d = reinterpret_cast<uint32_t*>(region + slot_words_of(qd));
+    jmax = 2 * sw - 1;
+  };
+  uint32_t len = encode_block4<S, REV, HALF>(place, lut, tab, X, region, kBlocks4PerWave * a.swp, v, cp,
                                              [&](S (&rr)[64]) {
                                                if (valid) {
                                                  gather3<S, VEC>(rr, data, g, ps);
@@ -96,19 +234,31 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
                                                    rr[i] = 0;
                                                }
                                              });
+  ZFP_TR4(3);
   len = valid ? len : 0u;
-  const bool over = a.ovf && len > a.cap_bits;  // quad-uniform
+  const uint32_t cap = slot_cap_bits4(sw);
+  const bool over = a.ovf && len > cap;  // quad-uniform
   const uint32_t lq = r == 0u ? len : 0u;  // the quad's lanes agree on len
   const uint32_t incl = wave_incl_scan(lq);
   const uint32_t total = __shfl(incl, 63, 64);
   if (r == 0u) {
     off[qd] = incl - lq;
-    wrt[qd] = over ? a.cap_bits : (len < 64 * a.swp ? len : 64 * a.swp);
+    wrt[qd] = wrt_of(len, sw, cap, over);
   }
+  // Every block fits its slot (wave-uniform; not so only when a block overflows
+  // a short slot or minbits pads past it): the wave compacts its slots in LDS
+  // while its predecessors finish, publishing its aggregate first, and writes
+  // the stream words as whole funnel-shifted words once its offset is known.
+  const bool simple = __builtin_amdgcn_ballot_w64(live && (over || (r == 0u && wrt_of(len, sw, cap, over) != len))) == 0;
+  if (live && a.var)
+    lookback_publish(a.status, w, total);
+  __syncthreads();  // off / wrt
+  if (live && simple)
+    compact_wave4<sizeof(S) == 4 ? 3 : 5>(region, off, wrt, [&](uint32_t l) { return region + slot_words_of(l); });
   uint64_t start = 0;
   if (!live) {
   } else if (a.var) {
-    start = lookback_wave(a.status, w, total, a.error);
+    start = lookback_walk(a.status, w, total, a.error);
     if (a.idx_len && valid && r == 0u)
       a.idx_len[b] = (uint16_t)len;
     if (lane == 0) {
@@ -120,6 +270,7 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   } else {
     start = first * (uint64_t)a.maxbits;
   }
+  ZFP_TR4(4);
   if (over && r == 0u) {
     const uint32_t k = take_overflow_slot(a);
     if (k != kNoSlot)
@@ -128,7 +279,16 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   __syncthreads();
   if (!live)
     return;
-  pack_wave<kBlocks4PerWave, false>(a, region, off, wrt, nullptr, w, start, total);
+  if (simple)
+    copy_out_wave(a, region, w, start, total);
+  else
+    pack_wave<kBlocks4PerWave, false>(a, region, off, wrt, nullptr, w, start, total,
+                                      [&](uint32_t l) { return region + slot_words_of(l); });
+#ifdef ZFP_EXP4_TRACE
+  __builtin_amdgcn_s_waitcnt(0);
+  ZFP_TR4(5);
+  if (a.trace && (w & 63) == 0 && lane == 0) a.trace[(w >> 6) * 8 + 6] = tr0;
+#endif
 }
 
 // Second pass of a short-slot encode4: the listed blocks (n entries, 16 per
@@ -166,9 +326,12 @@ __global__ __launch_bounds__(64) void encode4_patch(const S* __restrict__ data, 
       v[i] = 0;
   }
   __syncthreads();
-  uint32_t* d = reinterpret_cast<uint32_t*>(region + (size_t)qd * swp);
   Int* X = reinterpret_cast<Int*>(region) + (size_t)qd * kXStride;
-  const uint32_t len = encode_block4<S, REV>(d, 2 * swp - 1, lut, tab, X, region, kBlocks4PerWave * swp, v, cp,
+  auto place = [&](bool, uint32_t*& d, uint32_t& jmax) {
+    d = reinterpret_cast<uint32_t*>(region + (size_t)qd * swp);
+    jmax = 2 * swp - 1;
+  };
+  const uint32_t len = encode_block4<S, REV>(place, lut, tab, X, region, kBlocks4PerWave * swp, v, cp,
                                              [&](S (&rr)[64]) {
                                                if (valid) {
                                                  gather3<S, VEC>(rr, data, g, ps);

@@ -592,7 +592,7 @@ static uint32_t short_slot_words(const Plan& p)
 // slots sized for the worst case (f32 reversible: 8,462 bits, 17.3 KB) limits
 // the CU to 8 one-wave workgroups (2 waves per SIMD), where the registers allow
 // 3 (f32 reversible).  f32 reversible slots are cut to what 12 waves per CU
-// leave (93 words = 5,952 bits); a block that codes longer -- on the C5 field,
+// leave (93 words, 5,856 intact bits); a block that codes longer -- on the C5 field,
 // the blocks that fail the reversible cast test, about 8,300 bits each -- is
 // packed with its first bits and listed, and encode4_patch codes it again with
 // a full slot.  The overflow pool holds a quarter of the blocks (the round-4
@@ -602,11 +602,13 @@ static uint32_t short_slot_words(const Plan& p)
 // full slots (not measured).  ZFP_HIP_SLOT_WORDS=n forces n-word slots (tests
 // of the overflow and patch path), ZFP_HIP_FULL_SLOTS=1 full ones.
 // Data whose blocks mostly overflow (noise-like fields) would pay the redo on
-// every call: after a redo the next kFullSlotCalls4 calls of the process take
-// full slots directly, then short slots are tried again.
+// every call: after a redo the next kFullSlotCalls4 calls of the same thread
+// take full slots directly, then short slots are tried again.  The backoff is
+// per thread (a caller looping over its own noisy data), so calls of other
+// threads -- other zfp_parallel chunks, other devices -- are not slowed.
 constexpr uint32_t kShortSlotWords4 = 93;
 constexpr int kFullSlotCalls4 = 16;
-static std::atomic<int> g_full_slot_calls4{0};
+static thread_local int t_full_slot_calls4 = 0;
 template <typename S>
 static uint32_t short_slot_words4(const Plan& p)
 {
@@ -616,10 +618,11 @@ static uint32_t short_slot_words4(const Plan& p)
     return (uint32_t)atoi(e) | 1u;
   if (p.cp.minexp >= kMinExp)
     return ~0u;
-  int n = g_full_slot_calls4.load(std::memory_order_relaxed);
-  while (n > 0 && !g_full_slot_calls4.compare_exchange_weak(n, n - 1, std::memory_order_relaxed)) {
+  if (t_full_slot_calls4 > 0) {
+    t_full_slot_calls4--;
+    return ~0u;
   }
-  return n > 0 ? ~0u : kShortSlotWords4;
+  return kShortSlotWords4;
 }
 
 template <typename S>
@@ -668,16 +671,46 @@ static int run_encode4(Ctx* c, const Plan& p, const S* d_field, uint64_t* d_out,
       a.ovf_count = (uint32_t*)((char*)c->misc.p + 16);
       a.ovf_cap = (uint32_t)cap;
       a.ovf_swp = swp_full;
-      a.cap_bits = 32 * (2 * swp - 2);  // clamped writes of an outrun slot land in its last dword
+      a.cap_bits = slot_cap_bits4(swp);  // clamped writes of an outrun slot land in its last three dwords
     }
+#ifdef ZFP_EXP4_TRACE
+    const size_t ntr = (nwaves + 63) / 64 * 8;
+    uint64_t* d_tr = nullptr;
+    if (getenv("ZFP_HIP_TRACE4")) {
+      HIP_TRY(hipMalloc(&d_tr, ntr * 8));
+      HIP_TRY(hipMemsetAsync(d_tr, 0, ntr * 8, c->stream));
+    }
+    a.trace = d_tr;
+#endif
     HIP_TRY(hipEventRecord(c->ev[1], c->stream));
     launch_encode4_kernel<S>(c, p, d_field, dim3((unsigned)nwaves), lds, a, half);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->ev[2], c->stream));
+#ifdef ZFP_EXP4_TRACE
+    if (d_tr) {
+      std::vector<uint64_t> h(ntr);
+      HIP_TRY(hipMemcpyAsync(h.data(), d_tr, ntr * 8, hipMemcpyDeviceToHost, c->stream));
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      HIP_TRY(hipFree(d_tr));
+      // phases: 0 ticket, 1 gather landed, 2 cast+lifts+exchange, 3 transposes+coder, 4 look-back, 5 pack
+      double sum[6] = {0}, t0min = 1e30, t0max = 0;
+      size_t cnt = 0;
+      for (size_t i = 0; i + 8 <= ntr; i += 8) {
+        if (!h[i + 6]) continue;
+        cnt++;
+        uint64_t prev = 0;
+        for (int k = 0; k < 6; k++) { sum[k] += (double)(h[i + k] - prev); prev = h[i + k]; }
+        t0min = std::min(t0min, (double)h[i + 6]);
+        t0max = std::max(t0max, (double)h[i + 6]);
+      }
+      fprintf(stderr, "trace4 waves %zu (100 MHz ticks, mean): ticket %.1f gather %.1f cast+lift+xchg %.1f coder %.1f lookback %.1f pack %.1f | launch span %.0f\n",
+              cnt, sum[0] / cnt, sum[1] / cnt, sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt, t0max - t0min);
+    }
+#endif
     const int rc = finish_general(c, p, nwaves, d_out, g0, head, a, index, total_bits);
     if (rc == kRedoFullSlots) {
       if (!getenv("ZFP_HIP_SLOT_WORDS") && !getenv("ZFP_HIP_OVF_POOL"))
-        g_full_slot_calls4.store(kFullSlotCalls4, std::memory_order_relaxed);
+        t_full_slot_calls4 = kFullSlotCalls4;
       continue;
     }
     if (rc != 1 || !a.ovf)

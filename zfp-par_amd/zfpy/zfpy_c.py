@@ -179,16 +179,14 @@ def _out_buffer(size):
     return a, a.ctypes.data
 
 
-_bytes_raw = ctypes.pythonapi["PyBytes_FromStringAndSize"]
-_bytes_raw.restype = ctypes.c_void_p
-_bytes_raw.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
-_bytes_resize = ctypes.pythonapi._PyBytes_Resize
-_bytes_resize.restype = ctypes.c_int
-_bytes_resize.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_ssize_t]
-_py_decref = ctypes.pythonapi.Py_DecRef
-_py_decref.restype = None
-_py_decref.argtypes = [ctypes.c_void_p]
-_bytes_data_offset = bytes.__basicsize__ - 1  # ob_sval: the bytes' storage after the header
+# PyBytes_AsString: the storage of a bytes object.  The C API lets a caller fill
+# that storage only for an object it has just made with
+# PyBytes_FromStringAndSize(NULL, n) and not yet shared -- exactly how the
+# stream targets below are used.  Public API only: no private resize, no
+# assumption about the object layout.
+_bytes_addr = ctypes.pythonapi["PyBytes_AsString"]
+_bytes_addr.restype = ctypes.c_void_p
+_bytes_addr.argtypes = [ctypes.py_object]
 
 
 try:
@@ -218,36 +216,57 @@ def _make_resident(addr, size):
 
 
 def _bytes_target(size):
-    """(handle, address): a new, not yet shared bytes object of `size` bytes
-    that the library writes the stream into directly (no staging buffer, no
-    copy afterwards).  The handle owns the only reference; _bytes_take or
-    _bytes_drop must consume it."""
-    h = _bytes_raw(None, max(size, 1))
-    if not h:
-        raise MemoryError("bytes of %d" % size)
-    _make_resident(h + _bytes_data_offset, size)
-    return h, h + _bytes_data_offset
-
-
-def _bytes_take(h, n):
-    """The bytes object of handle h, shrunk to its first n bytes."""
-    ref = ctypes.c_void_p(h)
-    if _bytes_resize(ctypes.byref(ref), n) != 0:  # frees the object on failure
-        raise MemoryError("bytes resize to %d" % n)
-    out = ctypes.cast(ref, ctypes.py_object).value  # + 1 reference
-    _py_decref(ref)
-    return out
-
-
-def _bytes_drop(h):
-    _py_decref(h)
+    """(bytes object, address): a new bytes object of exactly `size` bytes (> 0)
+    that the library writes a stream into directly -- no staging buffer and no
+    copy afterwards.  Only for streams whose length is known before they are
+    written (fixed rate, _fixed_rate_size)."""
+    if size <= 0:
+        raise ValueError("stream target of %d bytes" % size)
+    out = _bytes_uninit(None, size)  # uninitialised storage, refcount 1, hash not yet cached
+    addr = _bytes_addr(out)
+    _make_resident(addr, size)
+    return out, addr
 
 
 def _bytes_from(addr, n):
     """A new bytes object holding n bytes from address addr, copied outside the GIL."""
-    out = _bytes_uninit(None, n)  # uninitialised storage, refcount 1, hash not yet cached
-    ctypes.memmove(ctypes.cast(ctypes.c_char_p(out), ctypes.c_void_p).value, addr, n)
+    out = _bytes_uninit(None, n)
+    if n:
+        ctypes.memmove(_bytes_addr(out), addr, n)
     return out
+
+
+def _header_bits(stream, field):
+    """Bits zfp_write_header(HEADER_FULL) writes for this stream and field (into scratch)."""
+    scratch = (ctypes.c_uint64 * 4)()
+    bs = _lib.stream_open(ctypes.addressof(scratch), ctypes.sizeof(scratch))
+    try:
+        _lib.zfp_stream_set_bit_stream(stream, bs)
+        _lib.zfp_stream_rewind(stream)
+        return int(_lib.zfp_write_header(stream, field, HEADER_FULL))
+    finally:
+        _lib.zfp_stream_set_bit_stream(stream, None)
+        _lib.stream_close(bs)
+
+
+def _fixed_rate_size(stream, field, nblocks, write_header):
+    """Exact byte length of a fixed-rate stream: the header, nblocks blocks of
+    maxbits bits each, flushed to a whole 64-bit word (zfp_compress's result)."""
+    hbits = 0
+    if write_header:
+        hbits = _header_bits(stream, field)
+        if hbits == 0:
+            raise RuntimeError("Failed to write header to stream")
+    mb, xb, mp, me = _u32(), _u32(), _u32(), _i32()
+    _lib.zfp_stream_params(stream, ctypes.byref(mb), ctypes.byref(xb), ctypes.byref(mp), ctypes.byref(me))
+    return (hbits + nblocks * int(xb.value) + 63) // 64 * 8
+
+
+def _nblocks(extents):
+    n = 1
+    for e in extents:
+        n *= (int(e) + 3) // 4
+    return n
 
 
 def _stream_bytes(obuf, n, index=None):
@@ -368,7 +387,6 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
     field = _make_field(ptr, dtype_to_ztype(dtype), list(reversed(shape)), list(reversed(strides)))
     stream = _lib.zfp_stream_open(None)
     bstream = None
-    target = None
     try:
         if device >= 0:
             _lib.zfp_stream_set_hip_device(stream, device)
@@ -376,6 +394,7 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
         maxsize = _lib.zfp_stream_maximum_size(stream, field)
         fixed = _fixed_rate(tolerance, rate)
         if fixed:
+            maxsize = _fixed_rate_size(stream, field, _nblocks(shape), write_header)
             target, buf = _bytes_target(maxsize)
         else:
             obuf, buf = _out_buffer(maxsize)
@@ -388,12 +407,11 @@ def compress_numpy(arr, tolerance=-1, rate=-1, precision=-1, write_header=True, 
         if n == 0:
             raise RuntimeError("Failed to write to stream")
         if fixed:
-            out, target = _bytes_take(target, n), None
-            return out
+            if n != maxsize:
+                raise RuntimeError("fixed-rate stream of %d bytes, %d expected" % (n, maxsize))
+            return target
         return _stream_bytes(obuf, n, _export_index(stream))
     finally:
-        if target is not None:
-            _bytes_drop(target)
         _lib.zfp_field_free(field)
         _lib.zfp_stream_close(stream)
         if bstream:
@@ -594,24 +612,29 @@ def _init_field_raw(py_raw_array, chunkit):
 def _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision, write_header, device, plain):
     """compress_numpy_portion's work.  plain=False: its return value (a ZfpBytes
     when the stream has a block index); plain=True: (plain bytes, index blob or
-    None), one GIL-free copy whatever the mode (zfp_parallel keeps the blobs)."""
+    None), one GIL-free copy at most whatever the mode (zfp_parallel keeps the
+    blobs).  A fixed-rate stream, whose length is known in advance, is written
+    straight into the returned bytes; a variable-rate one goes through the
+    thread's reusable staging buffer (its worst-case size is about the chunk's
+    uncompressed size, far more than the stream)."""
     if py_raw_array is None:
         raise TypeError("Input array cannot be None")
     _one_mode(tolerance, rate, precision)
     field = _init_field_raw(py_raw_array, chunkit)
     stream = _lib.zfp_stream_open(None)
     bstream = None
-    target = None
     try:
         if device >= 0:
             _lib.zfp_stream_set_hip_device(stream, device)
         _set_compression_mode(stream, type_none, chunkit.ndim, tolerance, rate, precision)
         ck = chunkit.chunk_ptr(ichunk)
-        maxsize = _lib.zfp_stream_maximum_size_chunk(stream, field, ck) + (HEADER_MAX_BITS + 63) // 64 * 8 + 8
         fixed = _fixed_rate(tolerance, rate)
-        if plain or fixed:
+        if fixed:
+            box = chunkit.boxes[ichunk][:chunkit.ndim]
+            maxsize = _fixed_rate_size(stream, field, _nblocks(e - f for f, e in box), write_header)
             target, buf = _bytes_target(maxsize)
         else:
+            maxsize = _lib.zfp_stream_maximum_size_chunk(stream, field, ck) + (HEADER_MAX_BITS + 63) // 64 * 8 + 8
             obuf, buf = _out_buffer(maxsize)
         bstream = _lib.stream_open(buf, maxsize)
         _lib.zfp_stream_set_bit_stream(stream, bstream)
@@ -621,17 +644,15 @@ def _compress_portion(py_raw_array, chunkit, ichunk, tolerance, rate, precision,
         n = _lib.zfp_compress_chunk(stream, ck, field)
         if n == 0:
             raise RuntimeError("Failed to write to stream")
+        if fixed:
+            if n != maxsize:
+                raise RuntimeError("fixed-rate chunk stream of %d bytes, %d expected" % (n, maxsize))
+            return (target, None) if plain else target  # no block index: the reference's plain bytes
         blob = _export_index(stream)
         if plain:
-            out, target = _bytes_take(target, n), None
-            return out, blob
-        if fixed:  # no block index: the reference's plain bytes
-            out, target = _bytes_take(target, n), None
-            return out
+            return _bytes_from(obuf.ctypes.data, n), blob
         return _stream_bytes(obuf, n, blob)
     finally:
-        if target is not None:
-            _bytes_drop(target)
         _lib.zfp_field_free(field)
         _lib.zfp_stream_close(stream)
         if bstream:

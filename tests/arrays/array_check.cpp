@@ -55,7 +55,7 @@ static int run(size_t nx, size_t ny, size_t nz, double rate, const char* in, con
       for (size_t i = 0; i < nx; i++)
         sum += (double)(T)a(i, j, k);
   // element writes: read-modify-writes of one element in each of 500 distinct
-  // random blocks, then whole rows of blocks in raster order -- every block's
+  // random blocks, then whole blocks one after another -- every block's
   // writes fall in one cache residency, in the reference's direct-mapped block
   // cache (cache.hpp) and in the line cache of zfp::hip alike (a block evicted
   // between two writes takes two lossy round trips, and the two caches evict
@@ -73,12 +73,13 @@ static int run(size_t nx, size_t ny, size_t nz, double rate, const char* in, con
     t++;
     a(i, j, k) = (T)(0.5 * (double)(T)a(i, j, k) + (double)(i + j + k));
   }
-  const size_t k0 = nz > 8 ? nz - 8 : 0;  // the last z layers: blocks the scattered writes left
-  for (size_t k = k0; k < nz; k++)
-    for (size_t j = 0; j < ny; j++)
-      for (size_t i = 0; i < nx; i++)
-        if (!hit[i / 4 + bx * (j / 4 + by * (k / 4))])
-          a(i, j, k) += (T)1;
+  // the last two z layers of blocks, block after block (each block's 64 writes in a row)
+  for (size_t b = (bz > 2 ? bz - 2 : 0) * bx * by; b < bx * by * bz; b++)
+    if (!hit[b])
+      for (size_t k = 4 * (b / (bx * by)); k < nz && k < 4 * (b / (bx * by)) + 4; k++)
+        for (size_t j = 4 * (b / bx % by); j < ny && j < 4 * (b / bx % by) + 4; j++)
+          for (size_t i = 4 * (b % bx); i < nx && i < 4 * (b % bx) + 4; i++)
+            a(i, j, k) += (T)1;
   put((pre + ".elem.z").c_str(), a.compressed_data(), a.compressed_size());
   a.get(out.data());
   put((pre + ".elem.raw").c_str(), out.data(), n * sizeof(T));

@@ -18,7 +18,7 @@ int main(int argc, char** argv)
   srand(1);
   long same = 0, hist_full[40] = {0}, hist_prec[40] = {0};
   double bits_same = 0, bits_not = 0, full_planes = 0, planes = 0;
-  long over93 = 0; static long lenhist_same[40], lenhist_not[40]; long wave_ns = 0, wave_cnt = 0; int wns = 0;
+  long over93 = 0; static uint32_t wu[16][256]; static int wprec[16]; static long cls[3], sec_hist[10], sec_wmax_hist[10], sec_fine[8]; double ext16 = 0, ext32 = 0, dec_it = 0, dec_win = 0, dec_seg = 0, gplanes = 0; static long lenhist_same[40], lenhist_not[40]; long wave_ns = 0, wave_cnt = 0; int wns = 0;
   uint64_t scratch[700];
   double wmaxprec = 0, wminfull = 0, wmaxnf = 0; int wmax = 0, wminf = 99, wnf = 0;
   for (int s = 0; s < samples; s++) {
@@ -51,6 +51,49 @@ int main(int argc, char** argv)
     for (int i = 0; i < 256; i++) { u[i] = oz_to_nb_f(q[oz_perm4[i]]); all |= u[i]; }
     int prec = all ? 32 - __builtin_ctz(all) : 1;
     hist_prec[prec]++;
+    memcpy(wu[s % 16], u, sizeof u); wprec[s % 16] = prec;
+    if (s % 16 == 15) {
+      /* per plane of the wave: does some lane (block q, segment r) have xs >= 2^16 / 2^32 */
+      uint32_t nn[16] = {0}, nk[16] = {0};
+      for (int k = 31; k >= 0; k--) {
+        int any = 0, e16 = 0, e32 = 0;
+        for (int q = 0; q < 16; q++) {
+          if (k < 32 - wprec[q]) continue;
+          any = 1;
+          for (int r = 0; r < 4; r++) {
+            int base = 64 * r, nr = (int)nn[q] - base; nr = nr < 0 ? 0 : nr > 64 ? 64 : nr;
+            uint64_t P = 0;
+            for (int j = 0; j < 64; j++) P |= (uint64_t)((wu[q][base + j] >> k) & 1) << j;
+            uint64_t xs = nr < 64 ? P >> nr : 0;
+            if (xs >> 16) e16 = 1;
+            if (xs >> 32) e32 = 1;
+          }
+          for (int i = 255; i >= (int)nn[q]; i--) if ((wu[q][i] >> k) & 1) { nn[q] = i + 1; break; }
+        }
+        if (any) { gplanes++; ext16 += e16; ext32 += e32; }
+        /* decode cost of this plane: serial group-test iterations (max over quads) and, for a
+           windowed parse, new ones per 128-bit window of the group bits (max over lanes) */
+        int it_max = 0, win_max = 0, seg_max = 0, sec_wmax = 0, anyone = 0, anylong = 0;
+        for (int q = 0; q < 16; q++) {
+          if (k < 32 - wprec[q] || nk[q] >= 256) continue;
+          uint32_t n0 = nk[q], tpos = 0, it = 1, cnt[5] = {0}, segc[4] = {0};
+          for (uint32_t i = n0; i < 256; i++) {
+            int b = (wu[q][i] >> k) & 1;
+            int rest = 0;
+            for (uint32_t j = i; j < 256; j++) rest |= (wu[q][j] >> k) & 1;
+            if (!rest) break;
+            if (b) { cnt[tpos / 128 < 4 ? tpos / 128 : 4]++; segc[i / 64]++; it++; tpos += 2; nk[q] = i + 1; } else tpos++;
+          }
+          if (it > it_max) it_max = it;
+          if (it > 1) { anyone = 1; if (tpos + 1 > 62 || nk[q] == 256) anylong = 1; }
+          /* section bits after the lead test: tokens up to the stop + the stop test */
+          if (it > 1) { uint32_t sl = tpos + 1; sec_hist[sl / 64 < 9 ? sl / 64 : 9]++; if ((int)sl > sec_wmax) sec_wmax = sl; }
+          for (int w = 0; w < 5; w++) if ((int)cnt[w] > win_max) win_max = cnt[w];
+          for (int w = 0; w < 4; w++) if ((int)segc[w] > seg_max) seg_max = segc[w];
+        }
+        if (any) { cls[anyone + anylong]++; sec_wmax_hist[sec_wmax / 64 < 9 ? sec_wmax / 64 : 9]++; if (sec_wmax < 64) sec_fine[sec_wmax / 8]++; dec_it += it_max; dec_win += win_max; dec_seg += seg_max; }
+      }
+    }
     /* n after each plane: the top one's index + 1 */
     uint32_t nn = 0; int full = 0;
     for (int k = 31; k >= 32 - prec; k--) {
@@ -74,6 +117,14 @@ int main(int argc, char** argv)
   printf("waves with a not-same block: %.1f%%\n", 100.0 * wave_ns / wave_cnt);
   printf("same len hist (256-bit bins):"); for (int i = 0; i < 40; i++) if (lenhist_same[i]) printf(" %d:%ld", i, lenhist_same[i]);
   printf("\nnot-same len hist:"); for (int i = 0; i < 40; i++) if (lenhist_not[i]) printf(" %d:%ld", i, lenhist_not[i]);
+  printf("\n");
+  printf("per wave: planes %.2f, planes taking ext (xs >= 2^16) %.2f, (xs >= 2^32) %.2f\n", gplanes / (samples / 16), ext16 / (samples / 16), ext32 / (samples / 16));
+  printf("per wave: serial group-test iterations %.1f (sum over planes of the max over quads), max new ones per 128-bit window %.1f, per 64-coefficient segment %.1f\n",
+         dec_it / (samples / 16), dec_win / (samples / 16), dec_seg / (samples / 16));
+  printf("section bits per block-plane (64-bit bins):"); for (int i = 0; i < 10; i++) printf(" %d:%ld", i, sec_hist[i]);
+  printf("\nper wave: planes with no new one %.2f, all sections in one 63-bit window %.2f, longer %.2f", cls[0] / (samples / 16.), cls[1] / (samples / 16.), cls[2] / (samples / 16.));
+  printf("\nwave max section bits < 64 (8-bit bins):"); for (int i = 0; i < 8; i++) printf(" %d:%ld", i, sec_fine[i]);
+  printf("\nwave max section bits per plane (64-bit bins):"); for (int i = 0; i < 10; i++) printf(" %d:%ld", i, sec_wmax_hist[i]);
   printf("\n");
   printf("prec hist:");
   for (int i = 0; i < 33; i++) if (hist_prec[i]) printf(" %d:%ld", i, hist_prec[i]);

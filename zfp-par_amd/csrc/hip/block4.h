@@ -577,7 +577,7 @@ __device__ __forceinline__ uint32_t encode_block4(Place&& place, const uint32_t*
     return end < cp.minbits ? cp.minbits : end;
   } else if constexpr (REV) {
     // reversible (revencodef.c:45-80)
-    int emax;
+    int emax = 0;
     bool fast = false;  // wave-uniform: no inf/NaN in any block of the wave (f32)
     if constexpr (sizeof(S) == 4) {
       // block maximum from integer maxima of the bit patterns (as
@@ -713,6 +713,13 @@ __device__ __forceinline__ uint32_t encode_block4(Place&& place, const uint32_t*
 // Decode the quad's block (invalid quads decode nothing but take part in the
 // wave-wide exchange); lane r receives slice w = r.  Returns the block's length
 // in bits including minbits padding (0 for an invalid quad), the encoder's.
+#ifdef ZFP_EXP4_TRACE
+__shared__ uint64_t zfp_dmarks[4];  // experiment: phase clocks of decode_block4 (lane 0)
+#define ZFP_DEC4_MARK(i) do { if (threadIdx.x == 0) zfp_dmarks[i] = wall_clock64(); } while (0)
+#else
+#define ZFP_DEC4_MARK(i) ((void)0)
+#endif
+
 template <typename S, bool REV, bool HALF = false>
 __device__ __forceinline__ uint32_t decode_block4(WordReader& rd, S (&v)[64], const CodecParams& cp,
                                                   typename Traits<S>::Int* X, const uint32_t* tab, bool valid)
@@ -778,13 +785,17 @@ __device__ __forceinline__ uint32_t decode_block4(WordReader& rd, S (&v)[64], co
       used = bits + decode_planes4<PREC>(rd, cp.maxbits - bits, prec, P);
       used = used < cp.minbits ? cp.minbits : used;
       pin_registers(P);
+      ZFP_DEC4_MARK(0);
       if constexpr (PREC == 32)
         coeffs_from_planes<false>(q, P);
       else
         coeffs_from_planes<false>(q, P, prec > 32);
     }
+    ZFP_DEC4_MARK(1);
     exchange_inv<REV, HALF>(q, X, tab);
+    ZFP_DEC4_MARK(2);
     xform<3, true, REV>(q);
+    ZFP_DEC4_MARK(3);
     if (REV && kind == 2u) {
 #pragma unroll
       for (int i = 0; i < 64; i++) {

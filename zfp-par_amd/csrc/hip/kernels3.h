@@ -721,6 +721,9 @@ struct DecodeArgs {
   // Equal lengths for every block prove the index right: block 0 starts at the
   // stream start, and each next start is the previous start plus its length.
   uint32_t* idx_bad;
+#ifdef ZFP_EXP4_TRACE
+  uint64_t* trace;  // experiment: per-phase clocks of every 64th wave (decode4)
+#endif
 };
 
 // Copy n 64-bit items to LDS, item t = lane + 64 i per lane: U loads are issued

@@ -52,39 +52,53 @@ struct OvfEntry {
 // In-place compaction of a wave's 16 slots into one bit string in LDS (local
 // bit 0 = the wave's first block), before its stream offset is known: block q
 // (wrt[q] bits at bit 0 of slot_of(q)) moves to local bit off[q], one block
-// after another.  Safe in place when every block fits its slot (the caller's
-// `simple` test): block q's destination ends at off[q + 1] <= 64 x the words
-// of slots 0..q, i.e. before slot q + 1, and within a block every lane reads
-// its words before any lane writes.  A block's first word ORs onto the end of
-// the previous block; every other word is stored whole (zero past the block).
-// NT: words per lane of the longest slot (f32: 136 words, f64: 263).
+// after another, as funnel-shifted dwords.  Safe in place when every block fits
+// its slot (the caller's `simple` test): block q's destination ends at
+// off[q + 1] <= 64 x the words of slots 0..q, i.e. before slot q + 1, and within
+// a block every lane reads its dwords before any lane writes.  The last dword
+// is masked to the block's bits (a budget cut leaves the rest of the cut plane
+// in the slot); the first dword ORs onto the end of the previous block.  NT: dwords per lane of the longest slot (f32: 272 dwords, f64: 526).
 template <int NT, typename SlotOf>
 __device__ __forceinline__ void compact_wave4(uint64_t* region, const uint32_t* off, const uint32_t* wrt,
                                               SlotOf&& slot_of)
 {
   const uint32_t lane = threadIdx.x & 63u;
+  uint32_t* dst0 = reinterpret_cast<uint32_t*>(region);
   for (uint32_t q = 0; q < kBlocks4PerWave; q++) {
-    const uint32_t L = wrt[q], D = off[q];
-    const uint64_t* src = slot_of(q);
-    const uint32_t d0 = D & 63u, nwq = (d0 + L + 63u) >> 6;
-    uint64_t v[NT];
+    // wave-uniform block geometry in scalar registers
+    const uint32_t L = (uint32_t)__builtin_amdgcn_readfirstlane((int)wrt[q]);
+    const uint32_t D = (uint32_t)__builtin_amdgcn_readfirstlane((int)off[q]);
+    const uint32_t d = D & 31u, nd = (d + L + 31u) >> 5;
+    // dword k of the destination holds block bits [32 k - d, 32 k - d + 32):
+    // alignbit(s[k], s[k - 1], 32 - d), read as the pair at src - 1 (d == 0:
+    // the pair at src, shift 0)
+    const uint32_t* src = reinterpret_cast<const uint32_t*>(slot_of(q)) - (d ? 1 : 0);
+    const uint32_t sh = (32u - d) & 31u;
+    // the last dword keeps the block's bits only: past a budget cut the slot
+    // holds the rest of the cut plane
+    const uint32_t valid = d + L - 32u * (nd - 1u);  // 1 .. 32
+    const uint32_t last_mask = valid >= 32u ? ~0u : (1u << valid) - 1u;
+    uint32_t* dst = dst0 + (D >> 5);
+    uint32_t v[NT];
 #pragma unroll
     for (int t = 0; t < NT; t++) {
-      const uint32_t k = lane + 64u * t;
-      const int64_t lo = (int64_t)k * 64 - d0;  // block bit at the word's bit 0
-      const int64_t x0 = lo > 0 ? lo : 0, x1 = lo + 64 < (int64_t)L ? lo + 64 : (int64_t)L;
-      v[t] = (k < nwq && x0 < x1) ? slot_bits(src, (uint32_t)x0, (uint32_t)(x1 - x0)) << (x0 - lo) : 0ull;
+      if (64u * t < nd) {
+        const uint32_t k = lane + 64u * t;
+        uint32_t lo = src[k], hi = src[k + 1];
+        if (t == 0)
+          lo = k == 0 && d ? 0u : lo;  // nothing below the block's first bit
+        v[t] = __builtin_amdgcn_alignbit(hi, lo, sh) & (k == nd - 1u ? last_mask : ~0u);
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the block's reads have returned
     __builtin_amdgcn_wave_barrier();
-    uint64_t* dst = region + (D >> 6);
 #pragma unroll
     for (int t = 0; t < NT; t++) {
-      const uint32_t k = lane + 64u * t;
-      if (k < nwq) {
-        if (k == 0 && d0)
-          dst[0] |= v[t];
-        else
+      if (64u * t < nd) {
+        const uint32_t k = lane + 64u * t;
+        if (t == 0 && k == 0 && d)
+          dst[0] |= v[t];  // onto the end of the previous block (same wave: in order)
+        else if (k < nd)
           dst[k] = v[t];
       }
     }
@@ -94,9 +108,12 @@ __device__ __forceinline__ void compact_wave4(uint64_t* region, const uint32_t* 
 }
 
 // Copy-out of a compacted wave (local words loc[0 ..]) to its stream bits
-// [G, G + total), G = g0 + start: every output word is a funnel shift of two
-// local words; the first and last word (shared with the neighbouring waves) go
-// to the partials for the fix-up kernels, as in pack_wave.
+// [G, G + total), G = g0 + start.  Output dword e holds local bits [32 e - r0,
+// 32 e - r0 + 32) = alignbit(Ld[e - j + 1], Ld[e - j], 32 j - r0), j = ceil(r0 /
+// 32) (as encode3_aligned's copy-out).  Each lane writes a pair of output words
+// aligned to 16 bytes in memory; the first and last word (shared with the
+// neighbouring waves) go to the partials for the fix-up kernels, as in
+// pack_wave.
 __device__ __forceinline__ void copy_out_wave(const GeneralArgs& a, const uint64_t* loc, uint64_t w, uint64_t start,
                                               uint32_t total)
 {
@@ -106,21 +123,45 @@ __device__ __forceinline__ void copy_out_wave(const GeneralArgs& a, const uint64
   const uint32_t r0 = (uint32_t)(G & 63);
   const uint64_t end = G + total;
   const uint32_t nw = (uint32_t)(((end - 1) >> 6) - W0 + 1);
-  const uint32_t nloc = (total + 63u) >> 6;
+  const uint32_t nld = (total + 31u) >> 5;  // local dwords that hold bits (the compaction wrote no others)
   const bool head_part = r0 != 0 || (nw == 1 && (end & 63));
   const bool tail_part = (end & 63) != 0;
-  for (uint32_t o = lane; o < nw; o += 64) {
-    const uint64_t cur = o < nloc ? loc[o] : 0ull;
-    const uint64_t prev = (o >= 1 && o - 1 < nloc) ? loc[o - 1] : 0ull;
-    const uint64_t val = r0 ? (cur << r0) | (prev >> (64 - r0)) : cur;
+  const uint32_t jj = (r0 + 31u) >> 5, sh = (32u * jj - r0) & 31u;
+  const uint32_t* Ld = reinterpret_cast<const uint32_t*>(loc);
+  auto ld = [&](int32_t i) -> uint32_t { return (i >= 0 && (uint32_t)i < nld) ? Ld[i] : 0u; };
+  // output word o at memory word W0 + o: pairs (o, o + 1) with W0 + o even
+  const uint32_t o0 = (uint32_t)((reinterpret_cast<uintptr_t>(a.out + W0) >> 3) & 1u);
+  auto emit = [&](uint32_t o, uint64_t val) {
     const bool head = o == 0 && head_part;
     const bool tail = o == nw - 1 && tail_part;
     if (head || tail)
       a.partials[2 * w + (o == 0 ? 0 : 1)] = Partial{W0 + o, val};
     else
       a.out[W0 + o] = val;
+  };
+  for (uint32_t c = lane; o0 + 2 * c < nw; c += 64) {
+    const uint32_t o = o0 + 2 * c;
+    const int32_t e = (int32_t)(2 * o) - (int32_t)jj;  // first input dword of output dword 2 o
+    const uint32_t x0 = ld(e), x1 = ld(e + 1), x2 = ld(e + 2), x3 = ld(e + 3), x4 = ld(e + 4);
+    const uint32_t y0 = __builtin_amdgcn_alignbit(x1, x0, sh), y1 = __builtin_amdgcn_alignbit(x2, x1, sh);
+    const uint32_t y2 = __builtin_amdgcn_alignbit(x3, x2, sh), y3 = __builtin_amdgcn_alignbit(x4, x3, sh);
+    const uint64_t v0 = ((uint64_t)y1 << 32) | y0, v1 = ((uint64_t)y3 << 32) | y2;
+    const bool whole = o + 1 < nw && !(o == 0 && head_part) && !(o + 1 == nw - 1 && tail_part);
+    if (whole) {
+      typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<u4*>(a.out + W0 + o) = u4{y0, y1, y2, y3};
+    } else {
+      emit(o, v0);
+      if (o + 1 < nw)
+        emit(o + 1, v1);
+    }
   }
   if (lane == 0) {
+    if (o0 == 1) {  // word 0 alone (before the first aligned pair)
+      const uint32_t y0 = __builtin_amdgcn_alignbit(ld(1 - (int32_t)jj), ld(-(int32_t)jj), sh);
+      const uint32_t y1 = __builtin_amdgcn_alignbit(ld(2 - (int32_t)jj), ld(1 - (int32_t)jj), sh);
+      emit(0, ((uint64_t)y1 << 32) | y0);
+    }
     if (!head_part)
       a.partials[2 * w].idx = kNoWord;
     if (!tail_part || nw == 1)
@@ -254,7 +295,7 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
     lookback_publish(a.status, w, total);
   __syncthreads();  // off / wrt
   if (live && simple)
-    compact_wave4<sizeof(S) == 4 ? 3 : 5>(region, off, wrt, [&](uint32_t l) { return region + slot_words_of(l); });
+    compact_wave4<sizeof(S) == 4 ? 5 : 9>(region, off, wrt, [&](uint32_t l) { return region + slot_words_of(l); });
   uint64_t start = 0;
   if (!live) {
   } else if (a.var) {
@@ -380,6 +421,12 @@ __global__ __launch_bounds__(64, kDec4Waves<S>) void decode4(S* __restrict__ dat
   const uint32_t lane = threadIdx.x;
   tab[lane] = kOrderTab4.t[lane];
   const uint64_t w = a.wave_list ? a.wave_list[blockIdx.x] : blockIdx.x;
+#ifdef ZFP_EXP4_TRACE
+  const uint64_t dt0 = wall_clock64();
+#define ZFP_DTR4(i) do { if (a.trace && !a.wave_list && (w & 63) == 0 && lane == 0) a.trace[(w >> 6) * 8 + (i)] = wall_clock64() - dt0; } while (0)
+#else
+#define ZFP_DTR4(i) ((void)0)
+#endif
   const uint64_t first = w * kBlocks4PerWave;
   const uint32_t qd = lane >> 2, r = lane & 3u;
   const uint64_t b = first + qd;
@@ -465,12 +512,18 @@ __global__ __launch_bounds__(64, kDec4Waves<S>) void decode4(S* __restrict__ dat
         });
   }
   __syncthreads();
+  ZFP_DTR4(0);
   WordReader rd;
   rd.w = rbase;
   rd.pos = rpos;
   S v[64];
   Int* X = reinterpret_cast<Int*>(region) + (size_t)(HALF ? (qd & 7u) : qd) * kXStride;
   const uint32_t used = decode_block4<S, REV, HALF>(rd, v, cp, X, tab, valid);
+  ZFP_DTR4(1);
+#ifdef ZFP_EXP4_TRACE
+  if (a.trace && !a.wave_list && (w & 63) == 0 && lane == 0)
+    for (int i = 0; i < 4; i++) a.trace[(w >> 6) * 8 + 2 + i] = zfp_dmarks[i] - dt0;
+#endif
   if (a.idx_bad && valid && r == 0u && used != len)
     atomicOr(a.idx_bad, 1u);
   if (!valid)
@@ -478,6 +531,13 @@ __global__ __launch_bounds__(64, kDec4Waves<S>) void decode4(S* __restrict__ dat
   const BlockPos p = block_pos(g, b, 4);
   if ((int)r < p.cnt[3])
     scatter3<S, VEC>(v, data, g, slice_pos(g, p, (int)r));
+#ifdef ZFP_EXP4_TRACE
+  __builtin_amdgcn_s_waitcnt(0);
+  if (a.trace && !a.wave_list && (w & 63) == 0 && lane == 0) {
+    a.trace[(w >> 6) * 8 + 6] = dt0;
+    a.trace[(w >> 6) * 8 + 7] = wall_clock64() - dt0;
+  }
+#endif
 }
 
 }  // namespace zfp_amd

@@ -885,6 +885,41 @@ static int run_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, 
     HIP_TRY(hipGetLastError());
     return 1;
   };
+#ifdef ZFP_EXP4_TRACE
+  const size_t ntr = (nwaves + 63) / 64 * 8;
+  uint64_t* d_tr = nullptr;
+  if (getenv("ZFP_HIP_TRACE4")) {
+    HIP_TRY(hipMalloc(&d_tr, ntr * 8));
+    HIP_TRY(hipMemsetAsync(d_tr, 0, ntr * 8, c->stream));
+  }
+  a.trace = d_tr;
+  struct TraceDump {
+    Ctx* c; uint64_t* d; size_t n;
+    ~TraceDump() {
+      if (!d) return;
+      std::vector<uint64_t> h(n);
+      if (hipMemcpyAsync(h.data(), d, n * 8, hipMemcpyDeviceToHost, c->stream) == hipSuccess &&
+          hipStreamSynchronize(c->stream) == hipSuccess) {
+        // slots: 0 staged, 2..5 decode_block4 marks (parse, planes->coefficients, exchange, lift),
+        // 1 decoded, 7 scattered
+        const int order[7] = {0, 2, 3, 4, 5, 1, 7};
+        double sum[7] = {0};
+        size_t cnt = 0;
+        for (size_t i = 0; i + 8 <= n; i += 8) {
+          if (!h[i + 6]) continue;
+          cnt++;
+          uint64_t prev = 0;
+          for (int k = 0; k < 7; k++) { sum[k] += (double)(h[i + order[k]] - prev); prev = h[i + order[k]]; }
+        }
+        if (cnt)
+          fprintf(stderr, "dtrace4 waves %zu (100 MHz ticks, mean): stage %.1f parse %.1f planes->coeffs %.1f "
+                  "exchange %.1f lift %.1f cast %.1f scatter %.1f\n", cnt, sum[0] / cnt, sum[1] / cnt,
+                  sum[2] / cnt, sum[3] / cnt, sum[4] / cnt, sum[5] / cnt, sum[6] / cnt);
+      }
+      (void)hipFree(d);
+    }
+  } dump{c, d_tr, ntr};
+#endif
   HIP_TRY(hipEventRecord(c->ev[1], c->stream));
   if (!packw) {
     if (!launch(0, dim3((unsigned)nwaves)))

@@ -80,6 +80,10 @@ class zfp_p:
         compress() returned."""
         if nthreads == -1:
             nthreads = cpu_count()
+        # drop the previous streams first: this object's references would
+        # otherwise keep them alive (peak memory: two sets of streams) until
+        # the new ones are assigned
+        self._compress_data, self._index_of = [], []
         tasks = [(i, tolerance, rate, precision) for i in range(self._chunkit.get_nchunks())]
 
         def one(i, tol, r, p):

@@ -27,3 +27,4 @@ for grp in "${PASSES[@]}"; do
   echo "pass $i ok"
 done
 python3 $R/tools/pmc_summary.py $OUT --bench $OUT/bench.json > $OUT/summary.txt
+rm -rf $OUT/p[0-9]*/  # raw counter CSVs: tens of MB, summarised above

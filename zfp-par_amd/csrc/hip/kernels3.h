@@ -511,12 +511,14 @@ __global__ __launch_bounds__(256, (kGenWaves<S, REV, HI>)) void encode3_general(
   // (inlined at both sites: the LDS copy must keep its ds_or writes)
   auto code = [&](OrSlot& os) __attribute__((always_inline)) -> uint32_t {
     S v[64];
-    BlockPos p = block_pos(g, b, D);
     if constexpr (D == 3 && !kIntField<S>) {
-      gather3<S, VEC>(v, data, g, p);
-      return encode_block3<S, REV, false, HI>(os, lut, v, cp, [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, p); });
+      gather3<S, VEC>(v, data, g, block_pos(g, b, D));
+      // the rare exact-cast path re-reads the block: its position is computed
+      // again there rather than held in registers across the coder
+      return encode_block3<S, REV, false, HI>(os, lut, v, cp,
+                                              [&](S (&r)[64]) { gather3<S, VEC>(r, data, g, block_pos(g, b, D)); });
     } else {
-      gather_n<S, D>(v, data, g, p);
+      gather_n<S, D>(v, data, g, block_pos(g, b, D));
       return encode_block_n<S, D, REV>(os, lut, v, cp);
     }
   };
@@ -852,17 +854,17 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
   __builtin_amdgcn_wave_barrier();
   if (!act)
     return;
-  const BlockPos p = block_pos(g, b, D);
-  // (inlined at both sites: the LDS copy must keep its ds_read accesses)
+  // (inlined at both sites: the LDS copy must keep its ds_read accesses; the
+  // block's position is computed after the decode, not held across it)
   auto dec = [&](WordReader& r) __attribute__((always_inline)) {
     S v[64];
     uint32_t used;
     if constexpr (D == 3 && !kIntField<S>) {
       used = decode_block3<S, REV, HI>(r, sq, v, cp);
-      scatter3<S, VEC>(v, data, g, p);
+      scatter3<S, VEC>(v, data, g, block_pos(g, b, D));
     } else {
       used = decode_block_n<S, D, REV>(r, sq, v, cp);
-      scatter_n<S, D>(v, data, g, p);
+      scatter_n<S, D>(v, data, g, block_pos(g, b, D));
     }
     // (every decoder, the short-slot f64 one included: at its register bound
     // the check moved its spills into the plane loop, C3 decode 4.94 -> 5.54

@@ -36,7 +36,7 @@ struct Case {
 template <typename S, int DIMS, bool REV>
 static bool run_scan(const Case& c, const std::vector<uint64_t>& words, uint64_t g0, uint64_t nb,
                      const std::vector<uint64_t>& truth, uint64_t seg_bits, uint64_t lead, uint32_t max_len,
-                     int* passes)
+                     int* passes, bool plausible = false)
 {
   ScanArgs a{};
   a.in = words.data();
@@ -58,6 +58,11 @@ static bool run_scan(const Case& c, const std::vector<uint64_t>& words, uint64_t
   a.moved = &moved;
   a.sp = ScanParams{c.p.minbits, c.p.maxbits, c.p.maxprec, c.p.minexp};
   uint64_t ring[kRing];
+  int32_t win[2];
+  if (plausible) {  // pass 1 starts its chains at plausible block starts (float blocks)
+    exp_window<S, DIMS, REV>(a, ring, win);
+    a.win = win;
+  }
   a.first = 1;
   for (uint64_t s = 0; s < a.nseg; s++)
     scan_segment<S, DIMS, REV>(a, s, ring);
@@ -179,6 +184,12 @@ static int run_case(const Case& c, std::mt19937_64& rng)
         if (!run_scan<S, DIMS, REV>(c, words, g0, nb, truth, seg, lead, max_len, &passes))
           fails++;
       }
+    // plausible chain starts in pass 1
+    for (uint64_t seg : {128ull, 2048ull, 1ull << 20}) {
+      int passes = 0;
+      if (!run_scan<S, DIMS, REV>(c, words, g0, nb, truth, seg, 0, max_len, &passes, true))
+        fails++;
+    }
   }
   printf("%s %s\n", c.name, fails ? "FAIL" : "ok");
   return fails;

@@ -46,5 +46,6 @@ ZFP_DECL4(double)
 // index scan pass (scan.h) for zfp_type `type` (1 int32, 2 int64, 3 float,
 // 4 double), dims 1..4
 void launch_scan_pass(int type, int dims, bool rev, dim3 grid, hipStream_t stream, const ScanArgs& a);
+void launch_scan_window(int type, int dims, bool rev, hipStream_t stream, const ScanArgs& a, int32_t* win);
 
 }  // namespace zfp_amd

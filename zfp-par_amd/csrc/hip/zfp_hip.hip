@@ -1254,6 +1254,15 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
   a.x = xs;
   a.moved = moved;
   a.sp = ScanParams{p.cp.minbits, p.cp.maxbits, p.cp.maxprec, p.cp.minexp};
+  // float streams: pass 1 starts each chain at a plausible block start (scan.h);
+  // ZFP_HIP_SCAN_PLAUSIBLE=0 starts them at the segment's first bit instead
+  const char* pl = getenv("ZFP_HIP_SCAN_PLAUSIBLE");
+  if ((p.type == 3 || p.type == 4) && !(pl && pl[0] == '0')) {
+    int32_t* win = reinterpret_cast<int32_t*>(moved + 2);
+    launch_scan_window(p.type, p.dims, p.cp.minexp < kMinExp, c->stream, a, win);
+    HIP_TRY(hipGetLastError());
+    a.win = win;
+  }
   launch_scan_dispatch(c, p, a);
   HIP_TRY(hipGetLastError());
   a.first = 0;

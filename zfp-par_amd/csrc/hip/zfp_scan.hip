@@ -28,6 +28,39 @@ static void scan_typed(int dims, bool rev, dim3 grid, hipStream_t st, const Scan
   }
 }
 
+template <typename S>
+static void window_typed(int dims, bool rev, hipStream_t st, const ScanArgs& a, int32_t* win)
+{
+  const dim3 one(1), block(64);
+  switch (dims) {
+    case 1:
+      if (rev) hipLaunchKernelGGL((scan_window<S, 1, true>), one, block, 0, st, a, win);
+      else hipLaunchKernelGGL((scan_window<S, 1, false>), one, block, 0, st, a, win);
+      break;
+    case 2:
+      if (rev) hipLaunchKernelGGL((scan_window<S, 2, true>), one, block, 0, st, a, win);
+      else hipLaunchKernelGGL((scan_window<S, 2, false>), one, block, 0, st, a, win);
+      break;
+    case 3:
+      if (rev) hipLaunchKernelGGL((scan_window<S, 3, true>), one, block, 0, st, a, win);
+      else hipLaunchKernelGGL((scan_window<S, 3, false>), one, block, 0, st, a, win);
+      break;
+    default:
+      if (rev) hipLaunchKernelGGL((scan_window<S, 4, true>), one, block, 0, st, a, win);
+      else hipLaunchKernelGGL((scan_window<S, 4, false>), one, block, 0, st, a, win);
+      break;
+  }
+}
+
+// the exponent window of pass 1's plausible chain starts (float types only)
+void launch_scan_window(int type, int dims, bool rev, hipStream_t stream, const ScanArgs& a, int32_t* win)
+{
+  if (type == 3)
+    window_typed<float>(dims, rev, stream, a, win);
+  else if (type == 4)
+    window_typed<double>(dims, rev, stream, a, win);
+}
+
 void launch_scan_pass(int type, int dims, bool rev, dim3 grid, hipStream_t stream, const ScanArgs& a)
 {
   switch (type) {

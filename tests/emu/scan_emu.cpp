@@ -58,7 +58,7 @@ static bool run_scan(const Case& c, const std::vector<uint64_t>& words, uint64_t
   a.moved = &moved;
   a.sp = ScanParams{c.p.minbits, c.p.maxbits, c.p.maxprec, c.p.minexp};
   uint64_t ring[kRing];
-  int32_t win[2];
+  int32_t win[3];
   if (plausible) {  // pass 1 starts its chains at plausible block starts (float blocks)
     exp_window<S, DIMS, REV>(a, ring, win);
     a.win = win;

@@ -167,6 +167,48 @@ int main(int argc, char** argv)
     printf("window [%d, %d] K=%d: first plausible start %.0f bits on, true %.1f%%, %.2f reads and %.3f block parses per searched bit\n",
            emin - 16, emax + 16, K, (double)dist / tries, 100.0 * hits / tries, (double)reads / dist, (double)parses / dist);
   }
+  // with a precision window too (reversible: the first 32 blocks' precisions -2),
+  // and the bits the deep checks parse
+  int pmin = 99;
+  {
+    CountReader r7{words.data(), words.size()};
+    for (int b = 0; b < 32; b++) {
+      const uint64_t h = r7.peek(starts[b]);
+      if (h & 1) { const int pr = (int)(((h >> 1) & 1) ? ((h >> 2) & 31) : ((h >> 10) & 31)) + 1; pmin = std::min(pmin, pr); }
+    }
+  }
+  auto head_ok2 = [&](uint64_t h) {
+    if (!(h & 1)) return false;
+    if (!((h >> 1) & 1)) {
+      const int e = (int)((h >> 2) & 0xff);
+      const int pr = (int)((h >> 10) & 31) + 1;
+      return e >= emin - 16 && e <= emax + 16 && pr >= pmin - 2;
+    }
+    return (((h >> 2) & 31) + 1) == 32;
+  };
+  for (int K : {2, 3, 4}) {
+    srand(11);
+    uint64_t hits = 0, tries = 300, dist = 0, pbits = 0, parses = 0;
+    for (uint64_t t = 0; t < tries; t++) {
+      CountReader r5{words.data(), words.size()};
+      uint64_t q = (uint64_t)rand() % (bits - 300000), q0 = q;
+      for (;; q++) {
+        if (!head_ok2(r5.peek(q))) continue;
+        uint64_t c = q;
+        int ok = 1;
+        for (int k = 0; k < K && ok; k++) {
+          if (k && !head_ok2(r5.peek(c))) { ok = 0; break; }
+          const uint32_t l = scan_block<float, 4, true>(r5, c, sp);
+          c += l; pbits += l; parses++;
+        }
+        if (ok) break;
+      }
+      dist += q - q0;
+      hits += std::binary_search(starts.begin(), starts.end(), q);
+    }
+    printf("e and prec (>= %d) windows, K=%d: start %.0f bits on, true %.1f%%, deep checks parse %.1f bits per searched bit (%.3f blocks)\n",
+           pmin - 2, K, (double)dist / tries, 100.0 * hits / tries, (double)pbits / dist, (double)parses / dist);
+  }
   // false chains from random starts, each followed for 64 Kbit
   srand(5);
   uint64_t fr = 0, fb = 0, fbits = 0, fj = 0;

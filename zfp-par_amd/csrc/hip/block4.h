@@ -407,52 +407,6 @@ __device__ __forceinline__ uint32_t code_planes4(uint32_t* d, uint32_t jmax, con
   return p < lim ? p : lim;
 }
 
-#ifdef ZFP_ENC4_PREPASS
-// Experiment: the length code_planes4 will return, without writing (its dlen
-// recurrence alone), so a wave can publish its look-back aggregate before it codes.
-template <int PREC>
-__device__ __forceinline__ uint32_t planes_len4(uint32_t pos, uint32_t lim, uint32_t maxprec,
-                                                const uint32_t (&Pl)[PREC], const uint32_t (&Ph)[PREC])
-{
-  const uint32_t r = threadIdx.x & 3u;
-  const uint32_t base = 64u * r;
-  const uint32_t kmin = (uint32_t)PREC > maxprec ? (uint32_t)PREC - maxprec : 0u;
-  uint32_t m_odd, m_hi;
-  quad_excl_masks(m_odd, m_hi);
-  uint32_t p = pos, n = 0;
-  bool tail = false;
-#pragma unroll
-  for (int k = PREC - 1; k >= 0; k--) {
-    if (tail)
-      continue;
-    const bool act = p < lim && (uint32_t)k >= kmin;
-    const uint64_t am = lanes_ult(p, lim) & lanes_ule(kmin, (uint32_t)k);
-    if (am == 0)
-      break;
-    if ((am & lanes_ne(n, 256u)) == 0) {
-      // every active quad has all 256 significant: planes k .. kmin are 256 bits each
-      const uint32_t np = (uint32_t)k >= kmin ? (uint32_t)k - kmin + 1u : 0u;
-      p = act ? p + 256u * np : p;
-      tail = true;
-      continue;
-    }
-    const uint64_t P = ((uint64_t)Ph[k] << 32) | Pl[k];
-    const uint32_t nr = (uint32_t)min(max((int)(n - base), 0), 64);
-    const uint64_t xs = (act && nr < 64u) ? P >> nr : 0ull;
-    const uint32_t L = xs ? 64u - (uint32_t)__clzll((long long)xs) : 0u;
-    const uint32_t tb = L ? base + nr + L : 0u;
-    const uint32_t n1 = quad_max(max(tb, n));
-    uint32_t ctot;
-    quad_excl((uint32_t)__popcll(xs), ctot, m_odd, m_hi);
-    const uint32_t all = n1 == 256u ? 1u : 0u;
-    const uint32_t impl = n1 > n ? all : 0u;
-    p = act ? p + n1 + ctot + 1u - all - impl : p;
-    n = act ? n1 : n;
-  }
-  return p < lim ? p : lim;
-}
-#endif
-
 // Decoder twin (decode.c:122-173, 212-246): the quad parses the group tests
 // redundantly (same stream bits, same control flow), each lane keeping the
 // ones of its segment; verbatim bits are read per segment.  One iteration per
@@ -480,7 +434,6 @@ __device__ __forceinline__ uint32_t decode_planes4(WordReader& rd, uint32_t budg
       uint64_t x = seg.read(cnt);
       rd.skip(m);
       bits -= m;
-#ifdef ZFP_DEC4_LEAN
       while (n < 256u && bits) {
         // one window per group test: bit 0 the test, then the zeros up to the
         // next one; a run of zeros past the window's 63 bits reads the next 64
@@ -512,35 +465,6 @@ __device__ __forceinline__ uint32_t decode_planes4(WordReader& rd, uint32_t budg
           x |= 1ull << (n - base);
         n++;
       }
-#else
-      while (n < 256u && bits) {
-        bits--;
-        if (!rd.read1())
-          break;
-        for (;;) {  // zeros up to the next one, at most to coefficient 255 / the budget
-          const uint32_t lim = min(255u - n, bits);
-          const uint32_t z = ctz64(rd.peek64());  // 64: no one in the next 64 bits
-          if (z >= lim) {
-            rd.skip(lim);
-            bits -= lim;
-            n += lim;
-            break;
-          }
-          if (z < 64u) {
-            rd.skip(z + 1);
-            bits -= z + 1;
-            n += z;
-            break;
-          }
-          rd.skip(64);
-          bits -= 64;
-          n += 64;
-        }
-        if (n - base < 64u)
-          x |= 1ull << (n - base);
-        n++;
-      }
-#endif
       P[k] = x;
     }
   }
@@ -607,15 +531,10 @@ __device__ __forceinline__ int lossy_emax_cast4(int64_t (&q)[64], double (&v)[64
 // (d: the slot's dwords, jmax: its last dword); big: the block codes with the
 // reversible reinterpreted-bits header (the long ones, about 8,300 bits on
 // f32 data), so a kernel with short slots can give it a full one.
-struct NoPublish4 {
-  __device__ void operator()(uint32_t) const {}
-};
-
-template <typename S, bool REV, bool HALF = false, typename Place, typename Reload, typename Publish = NoPublish4>
+template <typename S, bool REV, bool HALF = false, typename Place, typename Reload>
 __device__ __forceinline__ uint32_t encode_block4(Place&& place, const uint32_t* lut, const uint32_t* tab,
                                                   typename Traits<S>::Int* X, uint64_t* region, uint32_t region_words,
-                                                  S (&v)[64], const CodecParams& cp, Reload&& reload,
-                                                  Publish&& publish = Publish{})
+                                                  S (&v)[64], const CodecParams& cp, Reload&& reload)
 {
   using T = Traits<S>;
   using Int = typename T::Int;
@@ -731,31 +650,6 @@ __device__ __forceinline__ uint32_t encode_block4(Place&& place, const uint32_t*
     place(!same, d, jmax);
     OrSlot os{reinterpret_cast<uint64_t*>(d), jmax};
     const uint32_t e = (uint32_t)(emax + T::kEbias);
-#ifdef ZFP_ENC4_PREPASS
-    {
-      const uint32_t hb = same ? 2 + kE : 2;
-      const uint32_t minb0 = cp.minbits - (hb < cp.minbits ? hb : cp.minbits);
-      UInt all0 = 0;
-#pragma unroll
-      for (int i = 0; i < 64; i++)
-        all0 |= ((UInt)q[i] + T::kNbMask) ^ T::kNbMask;
-      all0 = quad_or(all0);
-      uint32_t prec0 = all0 ? (uint32_t)(PREC - (sizeof(S) == 4 ? __builtin_ctz((uint32_t)all0)
-                                                                : __builtin_ctzll((uint64_t)all0)))
-                            : 0u;
-      if (prec0 > cp.maxprec) prec0 = cp.maxprec;
-      if (prec0 < 1) prec0 = 1;
-      if constexpr (PREC == 32)
-        planes_from_coeffs<false>(Pl, Ph, q);
-      else
-        planes_from_coeffs<false>(Pl, Ph, q, prec0 > 32);
-      pin_registers(Pl);
-      pin_registers(Ph);
-      uint32_t ib0 = planes_len4<PREC>(hb + T::kPbits, cp.maxbits, prec0, Pl, Ph) - hb;
-      if (ib0 < minb0) ib0 = minb0;
-      publish((same && !e) ? (1u < cp.minbits ? cp.minbits : 1u) : hb + ib0);
-    }
-#endif
     if (same && !e)
       return 1u < cp.minbits ? cp.minbits : 1u;  // a single 0 bit
     uint32_t bits;
@@ -779,14 +673,12 @@ __device__ __forceinline__ uint32_t encode_block4(Place&& place, const uint32_t*
     if (prec > cp.maxprec) prec = cp.maxprec;
     if (prec < 1) prec = 1;
     if (r == 0u) os.put32(bits, prec - 1);
-#ifndef ZFP_ENC4_PREPASS
     if constexpr (PREC == 32)
       planes_from_coeffs<false>(Pl, Ph, q);
     else
       planes_from_coeffs<false>(Pl, Ph, q, prec > 32);
     pin_registers(Pl);
     pin_registers(Ph);
-#endif
     const uint32_t end = code_planes4<PREC>(d, jmax, lut, bits + T::kPbits, cp.maxbits, prec, Pl, Ph);
     uint32_t ib = end - bits;
     if (ib < minb) ib = minb;

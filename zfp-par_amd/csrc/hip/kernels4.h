@@ -265,20 +265,6 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
     d = reinterpret_cast<uint32_t*>(region + slot_words_of(qd));
     jmax = 2 * sw - 1;
   };
-#ifdef ZFP_ENC4_PREPASS
-  // experiment: the aggregate published from the length pre-pass, before the coder
-  bool pre = false;
-  auto publish = [&](uint32_t l0) {
-    const uint32_t lq0 = (valid && r == 0u) ? l0 : 0u;
-    const uint32_t t0 = __shfl(wave_incl_scan(lq0), 63, 64);
-    if (live && a.var)
-      lookback_publish(a.status, w, t0);
-    pre = true;
-  };
-#else
-  auto publish = NoPublish4{};
-  constexpr bool pre = false;
-#endif
   uint32_t len = encode_block4<S, REV, HALF>(place, lut, tab, X, region, kBlocks4PerWave * a.swp, v, cp,
                                              [&](S (&rr)[64]) {
                                                if (valid) {
@@ -288,8 +274,7 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
                                                  for (int i = 0; i < 64; i++)
                                                    rr[i] = 0;
                                                }
-                                             },
-                                             publish);
+                                             });
   ZFP_TR4(3);
   len = valid ? len : 0u;
   const uint32_t cap = slot_cap_bits4(sw);
@@ -306,7 +291,7 @@ __global__ __launch_bounds__(64) void encode4(const S* __restrict__ data, Geomet
   // while its predecessors finish, publishing its aggregate first, and writes
   // the stream words as whole funnel-shifted words once its offset is known.
   const bool simple = __builtin_amdgcn_ballot_w64(live && (over || (r == 0u && wrt_of(len, sw, cap, over) != len))) == 0;
-  if (live && a.var && !__builtin_amdgcn_readfirstlane(pre))
+  if (live && a.var)
     lookback_publish(a.status, w, total);
   __syncthreads();  // off / wrt
   if (live && simple)

@@ -298,7 +298,7 @@ struct ScanArgs {
   uint64_t* x;           // per segment: exits after this pass
   uint32_t* moved;       // count of exits that moved in this pass
   ScanParams sp;
-  const int32_t* win;    // pass 1, float blocks: exponent window of plausible block starts (null: off)
+  const int32_t* win;    // pass 1, float blocks: plausible block starts' exponent window, min precision (null: off)
 };
 
 // ---------------------------------------------------------------------------
@@ -317,7 +317,7 @@ struct ScanArgs {
 constexpr int kPlausibleBlocks = 4;
 
 template <typename S, bool REV>
-__device__ __forceinline__ bool head_plausible(uint64_t h, int32_t elo, int32_t ehi)
+__device__ __forceinline__ bool head_plausible(uint64_t h, int32_t elo, int32_t ehi, int32_t pmin)
 {
   using T = Traits<S>;
   if (!(h & 1))
@@ -326,7 +326,8 @@ __device__ __forceinline__ bool head_plausible(uint64_t h, int32_t elo, int32_t 
     if ((h >> 1) & 1)  // reinterpreted bits: precision in the next kPbits
       return (uint32_t)((h >> 2) & ((1u << T::kPbits) - 1)) + 1 == (uint32_t)T::kIntPrec;
     const int32_t e = (int32_t)((h >> 2) & ((1u << T::kEbits) - 1));
-    return e >= elo && e <= ehi;
+    const int32_t pr = (int32_t)((h >> (2 + T::kEbits)) & ((1u << T::kPbits) - 1)) + 1;
+    return e >= elo && e <= ehi && pr >= pmin;
   } else {
     const int32_t e = (int32_t)((h >> 1) & ((1u << T::kEbits) - 1));
     return e >= elo && e <= ehi;
@@ -340,7 +341,7 @@ constexpr uint32_t kHeadBits = 2 + Traits<S>::kEbits + (REV ? Traits<S>::kPbits 
 // first plausible chain start in [lo, hi), else lo; leaves the ring at it
 template <typename S, int DIMS, bool REV>
 __device__ __forceinline__ uint64_t plausible_start(RingReader& rd, uint64_t lo, uint64_t hi, const ScanParams& sp,
-                                                    int32_t elo, int32_t ehi)
+                                                    int32_t elo, int32_t ehi, int32_t pmin)
 {
   constexpr uint32_t kStep = 64 - kHeadBits<S, REV>;
   for (uint64_t q = lo; q < hi; q += kStep) {
@@ -351,12 +352,12 @@ __device__ __forceinline__ uint64_t plausible_start(RingReader& rd, uint64_t lo,
     while (ones) {
       const uint32_t i = ctz64(ones);
       ones &= ones - 1;
-      if (!head_plausible<S, REV>(W >> i, elo, ehi))
+      if (!head_plausible<S, REV>(W >> i, elo, ehi, pmin))
         continue;
       uint64_t c = q + i;
       bool ok = true;
       for (int k = 0; k < kPlausibleBlocks && ok; k++) {
-        if (k && !head_plausible<S, REV>(rd.peek(c), elo, ehi))
+        if (k && !head_plausible<S, REV>(rd.peek(c), elo, ehi, pmin))
           ok = false;
         else
           c += scan_block<S, DIMS, REV>(rd, c, sp);
@@ -370,8 +371,9 @@ __device__ __forceinline__ uint64_t plausible_start(RingReader& rd, uint64_t lo,
   return lo;
 }
 
-// the exponent window of plausible starts: the range of the stream's first
-// 32 blocks' exponents, widened by 16 (empty when none carries one)
+// the window of plausible starts from the stream's first 32 blocks: their
+// exponents' range widened by 16 (empty when none carries one) and, for
+// reversible blocks with an exponent, their lowest precision less 2
 template <typename S, int DIMS, bool REV>
 __device__ __forceinline__ void exp_window(const ScanArgs& a, uint64_t* ring, int32_t* win)
 {
@@ -382,7 +384,7 @@ __device__ __forceinline__ void exp_window(const ScanArgs& a, uint64_t* ring, in
   rd.g0 = a.g0;
   rd.ring = ring;
   rd.start(0);
-  int32_t lo = 1 << 30, hi = -(1 << 30);
+  int32_t lo = 1 << 30, hi = -(1 << 30), pm = 1 << 30;
   uint64_t p = 0;
   for (int b = 0; b < 32 && p < a.limit; b++) {
     const uint64_t h = rd.peek(p);
@@ -390,11 +392,16 @@ __device__ __forceinline__ void exp_window(const ScanArgs& a, uint64_t* ring, in
       const int32_t e = (int32_t)((h >> (REV ? 2 : 1)) & ((1u << T::kEbits) - 1));
       lo = e < lo ? e : lo;
       hi = e > hi ? e : hi;
+      if (REV) {
+        const int32_t pr = (int32_t)((h >> (2 + T::kEbits)) & ((1u << T::kPbits) - 1)) + 1;
+        pm = pr < pm ? pr : pm;
+      }
     }
     p += scan_block<S, DIMS, REV>(rd, p, a.sp);
   }
   win[0] = lo <= hi ? lo - 16 : 1;
   win[1] = lo <= hi ? hi + 16 : 0;
+  win[2] = REV && lo <= hi ? pm - 2 : 0;
 }
 
 // One segment of a pass (one lane).
@@ -425,7 +432,7 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
   rd.ring = ring;
   if (e == ~0ull) {
     rd.start(lo);
-    e = plausible_start<S, DIMS, REV>(rd, lo, hi, a.sp, a.win[0], a.win[1]);
+    e = plausible_start<S, DIMS, REV>(rd, lo, hi, a.sp, a.win[0], a.win[1], a.win[2]);
   } else {
     rd.start(e);
   }

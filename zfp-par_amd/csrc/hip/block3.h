@@ -721,8 +721,10 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t*
     xform<3, true, false>(q);
     // f64: the lift finishes before the conversions start (interleaved, the two
     // need more than the 168 registers of three waves per SIMD and spill)
+#ifndef ZFP_C3_NOPIN
     if constexpr (sizeof(S) == 8)
       pin_registers(q);
+#endif
     inv_cast(v, q, emax);
   } else {
 #pragma unroll

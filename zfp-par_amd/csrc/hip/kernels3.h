@@ -771,7 +771,11 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
 #pragma unroll
   for (int k = 0; k < 4; k++)
     sq[lane + 64 * k] = squeeze_entry(lane + 64 * k);
+#ifdef ZFP_C3_VWV
+  const int wv = threadIdx.x >> 6;
+#else
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar registers
+#endif
   uint64_t* wslot = lds + (size_t)wv * 64 * a.swp;
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
   const uint64_t first = w * 64;

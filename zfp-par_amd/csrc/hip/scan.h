@@ -299,6 +299,9 @@ struct ScanArgs {
   uint32_t* moved;       // count of exits that moved in this pass
   ScanParams sp;
   const int32_t* win;    // pass 1, float blocks: plausible block starts' exponent window, min precision (null: off)
+  uint64_t* plaus;       // per segment: its pass-1 plausible start (~0: none); null: off
+  uint32_t refuse;       // phase A: refuse implausible chains at segments that keep their plausible chain
+  uint32_t* refused;     // count of refusals in this pass
 };
 
 // ---------------------------------------------------------------------------
@@ -338,11 +341,12 @@ __device__ __forceinline__ bool head_plausible(uint64_t h, int32_t elo, int32_t 
 template <typename S, bool REV>
 constexpr uint32_t kHeadBits = 2 + Traits<S>::kEbits + (REV ? Traits<S>::kPbits : 0);
 
-// first plausible chain start in [lo, hi), else lo; leaves the ring at it
+// first plausible chain start in [lo, hi) (found = true), else lo; leaves the ring at it
 template <typename S, int DIMS, bool REV>
 __device__ __forceinline__ uint64_t plausible_start(RingReader& rd, uint64_t lo, uint64_t hi, const ScanParams& sp,
-                                                    int32_t elo, int32_t ehi, int32_t pmin)
+                                                    int32_t elo, int32_t ehi, int32_t pmin, bool& found)
 {
+  found = true;
   constexpr uint32_t kStep = 64 - kHeadBits<S, REV>;
   for (uint64_t q = lo; q < hi; q += kStep) {
     const uint64_t W = rd.peek(q);
@@ -368,6 +372,7 @@ __device__ __forceinline__ uint64_t plausible_start(RingReader& rd, uint64_t lo,
     }
   }
   rd.start(lo);
+  found = false;
   return lo;
 }
 
@@ -421,9 +426,13 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
     e = lo > a.lead ? lo - a.lead : 0;  // lead-in start (0: the true chain)
   else
     e = a.xsnap[s - 1];
+  uint64_t es = ~0ull;  // phase A: the plausible start this segment's chain still begins at
   if (!a.first) {
-    if (e == a.entry_used[s])
+    const uint64_t cur = a.entry_used[s];
+    if (e == cur)
       return;  // this segment's chain already starts where the previous one exits
+    if (a.refuse && a.plaus && a.plaus[s] == cur && e < cur)
+      es = cur;
   }
   RingReader rd;
   rd.in = a.in;
@@ -432,7 +441,10 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
   rd.ring = ring;
   if (e == ~0ull) {
     rd.start(lo);
-    e = plausible_start<S, DIMS, REV>(rd, lo, hi, a.sp, a.win[0], a.win[1], a.win[2]);
+    bool found;
+    e = plausible_start<S, DIMS, REV>(rd, lo, hi, a.sp, a.win[0], a.win[1], a.win[2], found);
+    if (a.plaus)
+      a.plaus[s] = found ? e : ~0ull;
   } else {
     rd.start(e);
   }
@@ -456,7 +468,24 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
   uint64_t wi = lo >> 6;     // bitmap word being assembled
   uint64_t acc = 0;          // this chain's starts in word wi
   bool merged = false;
+  uint32_t odd = 0;          // blocks of this chain that do not look real (phase A)
   while (p < hi) {
+    if (es != ~0ull && p > es) {
+      // Phase A: the incoming chain passed this segment's plausible start
+      // without landing on it, so one of the two is false.  A chain that has
+      // already produced blocks that do not look real is taken to be the false
+      // one: the segment keeps its chain (the words this parse flushed lie
+      // below the plausible start, where that chain has no starts) and its
+      // exit.  Phase B (normal passes) settles any refusal that was wrong.
+      if (odd) {
+        for (uint64_t j = lo >> 6; j < wi; j++)
+          a.bm[j] = 0;
+        a.entry_used[s] = es;
+        atomicAdd(a.refused, 1u);
+        return;
+      }
+      es = ~0ull;
+    }
     const uint64_t pw = p >> 6;
     while (wi < pw) {
       a.bm[wi] = acc;
@@ -466,6 +495,10 @@ __device__ __forceinline__ void scan_segment(const ScanArgs& a, uint64_t s, uint
     const uint32_t sh = (uint32_t)(p & 63);
     const uint64_t old = check ? a.bm[wi] : 0ull;  // consumed after the parse below
     const uint64_t h = rd.peek(p);
+    if constexpr (!std::is_integral<S>::value) {
+      if (es != ~0ull && !head_plausible<S, REV>(h, a.win[0], a.win[1], a.win[2]))
+        odd++;
+    }
     if (runs && !(h & 1)) {
       // a run of zero blocks, one bit each, within this bitmap word
       uint32_t c = ctz64(h);

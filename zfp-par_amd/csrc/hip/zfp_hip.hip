@@ -1226,7 +1226,7 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
   const uint64_t nseg = (limit + seg - 1) / seg;
   const uint64_t bm_words = (limit + 63) / 64;
   const uint64_t ntiles = (bm_words + kTileWords - 1) / kTileWords;
-  if (!ensure(c->scan_bm, bm_words * 8) || !ensure(c->scan_seg, nseg * 3 * 8 + 64) ||
+  if (!ensure(c->scan_bm, bm_words * 8) || !ensure(c->scan_seg, nseg * 4 * 8 + 64) ||
       !ensure(c->scan_tiles, ntiles * 8 + 64) || !ensure(c->scan_pos, (nb + 1) * 8) ||
       !index_reserve(x, nb, nwaves))
     return 0;
@@ -1236,7 +1236,9 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
   uint64_t* used = (uint64_t*)c->scan_seg.p;
   uint64_t* xs = used + nseg;
   uint64_t* xsnap = xs + nseg;
-  uint32_t* moved = (uint32_t*)(xsnap + nseg);
+  uint64_t* plaus = xsnap + nseg;
+  uint32_t* moved = (uint32_t*)(plaus + nseg);
+  uint32_t* refused = moved + 1;
   HIP_TRY(hipMemsetAsync(bm, 0, bm_words * 8, c->stream));
   HIP_TRY(hipMemsetAsync(used, 0xff, nseg * 8, c->stream));
   ScanArgs a{};
@@ -1262,6 +1264,8 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
     launch_scan_window(p.type, p.dims, p.cp.minexp < kMinExp, c->stream, a, win);
     HIP_TRY(hipGetLastError());
     a.win = win;
+    a.plaus = plaus;
+    a.refused = refused;
   }
   launch_scan_dispatch(c, p, a);
   HIP_TRY(hipGetLastError());
@@ -1276,24 +1280,32 @@ static int scan_index(Ctx* c, const Plan& p, const uint64_t* d_in, uint64_t in_w
             (unsigned long long)seg, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tp).count());
     tp = std::chrono::steady_clock::now();
   }
+  // phase A (plausible starts only): passes that refuse implausible chains at
+  // segments still holding their plausible chain; phase B: ordinary passes,
+  // which settle whatever phase A left inconsistent (scan.h)
+  a.refuse = a.plaus ? 1u : 0u;
   for (;;) {
-    uint32_t host_moved = 0;
+    uint32_t host_cnt[2] = {0, 0};
     HIP_TRY(hipMemcpyAsync(xsnap, xs, nseg * 8, hipMemcpyDeviceToDevice, c->stream));
-    HIP_TRY(hipMemsetAsync(moved, 0, 4, c->stream));
+    HIP_TRY(hipMemsetAsync(moved, 0, 8, c->stream));
     launch_scan_dispatch(c, p, a);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(&host_moved, moved, 4, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(host_cnt, moved, 8, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
     passes++;
     if (trace) {
       const auto t = std::chrono::steady_clock::now();
-      fprintf(stderr, "scan: pass %d %.3f ms, %u exits moved\n", passes,
-              std::chrono::duration<double, std::milli>(t - tp).count(), host_moved);
+      fprintf(stderr, "scan: pass %d%s %.3f ms, %u exits moved, %u refused\n", passes, a.refuse ? " (A)" : "",
+              std::chrono::duration<double, std::milli>(t - tp).count(), host_cnt[0], host_cnt[1]);
       tp = t;
     }
-    if (!host_moved)
-      break;
-    if ((uint64_t)passes > nseg + 2)
+    if (!host_cnt[0]) {
+      if (!a.refuse || !host_cnt[1])
+        break;
+      a.refuse = 0;  // phase A settled with refusals outstanding: ordinary passes
+      continue;
+    }
+    if ((uint64_t)passes > 2 * nseg + 4)
       return fail("zfp_hip: index scan did not converge after %d passes", passes);
   }
   // bitmap -> positions -> index

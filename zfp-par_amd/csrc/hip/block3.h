@@ -644,15 +644,8 @@ __device__ __forceinline__ uint32_t encode_block3(OrSlot& w, const uint32_t* lut
 }
 
 // Decode one block; returns the number of bits consumed (incl. padding).
-struct NoUsed3 {
-  __device__ void operator()(uint32_t) const {}
-};
-
-// on_used(bits): called with the block's length as soon as it is parsed (the
-// decoders' index check), so the length is not held across the transform
-template <typename S, bool REV, bool HI = false, typename Used = NoUsed3>
-__device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t* sq, S (&v)[64], const CodecParams& cp,
-                                                  Used&& on_used = Used{})
+template <typename S, bool REV, bool HI = false>
+__device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t* sq, S (&v)[64], const CodecParams& cp)
 {
   using T = Traits<S>;
   using Int = typename T::Int;
@@ -668,7 +661,6 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t*
         r.skip(cp.minbits - bits);
         bits = cp.minbits;
       }
-      on_used(bits);
       return bits;
     }
     bits++;
@@ -686,7 +678,6 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t*
       r.skip(minb - ib);
       ib = minb;
     }
-    on_used(bits + ib);
     xform<3, true, true>(q);
     if (reinterp) {
 #pragma unroll
@@ -717,14 +708,7 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t*
       ib = minb;
     }
     bits += ib;
-    on_used(bits);
     xform<3, true, false>(q);
-    // f64: the lift finishes before the conversions start (interleaved, the two
-    // need more than the 168 registers of three waves per SIMD and spill)
-#ifndef ZFP_C3_NOPIN
-    if constexpr (sizeof(S) == 8)
-      pin_registers(q);
-#endif
     inv_cast(v, q, emax);
   } else {
 #pragma unroll
@@ -733,7 +717,6 @@ __device__ __forceinline__ uint32_t decode_block3(WordReader& r, const uint32_t*
       r.skip(cp.minbits - bits);
       bits = cp.minbits;
     }
-    on_used(bits);
   }
   return bits;
   }

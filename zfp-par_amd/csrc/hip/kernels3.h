@@ -771,11 +771,7 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
 #pragma unroll
   for (int k = 0; k < 4; k++)
     sq[lane + 64 * k] = squeeze_entry(lane + 64 * k);
-#ifdef ZFP_C3_VWV
   const int wv = threadIdx.x >> 6;
-#else
-  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar registers
-#endif
   uint64_t* wslot = lds + (size_t)wv * 64 * a.swp;
   const uint64_t w = (uint64_t)blockIdx.x * kWavesPerGroup + wv;
   const uint64_t first = w * 64;
@@ -856,38 +852,23 @@ __global__ __launch_bounds__(256, SHORT ? 3 : 1) void decode3(S* __restrict__ da
   __builtin_amdgcn_wave_barrier();
   if (!act)
     return;
-  // SHORT (f64 at its 168-register bound): the index length waits in LDS and
-  // the lane is counted again after the decode, so no per-lane value is held
-  // in registers across it (they would be the kernel's only spills)
-  if constexpr (SHORT)
-    sbit[threadIdx.x] = len;
   // (inlined at both sites: the LDS copy must keep its ds_read accesses; the
   // block's position is computed after the decode, not held across it)
   auto dec = [&](WordReader& r) __attribute__((always_inline)) {
     S v[64];
-    // the index check, as soon as the block is parsed
+    uint32_t used;
+    if constexpr (D == 3 && !kIntField<S>) {
+      used = decode_block3<S, REV, HI>(r, sq, v, cp);
+      scatter3<S, VEC>(v, data, g, block_pos(g, b, D));
+    } else {
+      used = decode_block_n<S, D, REV>(r, sq, v, cp);
+      scatter_n<S, D>(v, data, g, block_pos(g, b, D));
+    }
     // (every decoder, the short-slot f64 one included: at its register bound
     // the check moved its spills into the plane loop, C3 decode 4.94 -> 5.54
     // ms, until the rare branches were laid out cold: 4.84 ms, ZFP_RARE)
-    auto check = [&](uint32_t used) {
-      uint32_t ln = len;
-      if constexpr (SHORT)
-        ln = sbit[wv * 64 + __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u))];
-      if (a.idx_bad && used != ln)
-        atomicOr(a.idx_bad, 1u);
-    };
-    if constexpr (D == 3 && !kIntField<S>) {
-      decode_block3<S, REV, HI>(r, sq, v, cp, check);
-    } else {
-      check(decode_block_n<S, D, REV>(r, sq, v, cp));
-    }
-    uint64_t bb = b;
-    if constexpr (SHORT)
-      bb = first + __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    if constexpr (D == 3 && !kIntField<S>)
-      scatter3<S, VEC>(v, data, g, block_pos(g, bb, D));
-    else
-      scatter_n<S, D>(v, data, g, block_pos(g, bb, D));
+    if (a.idx_bad && used != len)
+      atomicOr(a.idx_bad, 1u);
   };
   if (SHORT && __any(over)) {
     if (over) {

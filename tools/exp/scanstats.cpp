@@ -186,12 +186,14 @@ int main(int argc, char** argv)
     }
     return (((h >> 2) & 31) + 1) == 32;
   };
-  for (int K : {2, 3, 4}) {
+  std::vector<uint64_t> lane_bits;
+  for (int K : {4}) {
     srand(11);
-    uint64_t hits = 0, tries = 300, dist = 0, pbits = 0, parses = 0;
+    uint64_t hits = 0, tries = 1000, dist = 0, pbits = 0, parses = 0;
     for (uint64_t t = 0; t < tries; t++) {
       CountReader r5{words.data(), words.size()};
       uint64_t q = (uint64_t)rand() % (bits - 300000), q0 = q;
+      const uint64_t pb0 = pbits;
       for (;; q++) {
         if (!head_ok2(r5.peek(q))) continue;
         uint64_t c = q;
@@ -204,10 +206,17 @@ int main(int argc, char** argv)
         if (ok) break;
       }
       dist += q - q0;
+      lane_bits.push_back(pbits - pb0);
       hits += std::binary_search(starts.begin(), starts.end(), q);
     }
     printf("e and prec (>= %d) windows, K=%d: start %.0f bits on, true %.1f%%, deep checks parse %.1f bits per searched bit (%.3f blocks)\n",
            pmin - 2, K, (double)dist / tries, 100.0 * hits / tries, (double)pbits / dist, (double)parses / dist);
+    std::sort(lane_bits.begin(), lane_bits.end());
+    if (!lane_bits.empty())
+      printf("   bits parsed per search: median %llu, p90 %llu, p99 %llu, max %llu\n",
+             (unsigned long long)lane_bits[lane_bits.size() / 2], (unsigned long long)lane_bits[lane_bits.size() * 9 / 10],
+             (unsigned long long)lane_bits[lane_bits.size() * 99 / 100], (unsigned long long)lane_bits.back());
+    lane_bits.clear();
   }
   // false chains from random starts, each followed for 64 Kbit
   srand(5);

@@ -341,21 +341,12 @@ __device__ __forceinline__ bool head_plausible(uint64_t h, int32_t elo, int32_t 
 template <typename S, bool REV>
 constexpr uint32_t kHeadBits = 2 + Traits<S>::kEbits + (REV ? Traits<S>::kPbits : 0);
 
-// Bits the candidate checks of one segment may parse before it gives up and
-// starts at its first bit: the checks parse garbage blocks, and on the C5 field
-// a search parses 28 Kbit at the median but 190 Kbit at p99 (tools/exp/
-// scanstats.cpp), which would set pass 1's time.
-#ifndef ZFP_SCAN_CHECK_BITS
-#define ZFP_SCAN_CHECK_BITS 65536
-#endif
-
 // first plausible chain start in [lo, hi) (found = true), else lo; leaves the ring at it
 template <typename S, int DIMS, bool REV>
 __device__ __forceinline__ uint64_t plausible_start(RingReader& rd, uint64_t lo, uint64_t hi, const ScanParams& sp,
                                                     int32_t elo, int32_t ehi, int32_t pmin, bool& found)
 {
   found = true;
-  uint64_t spent = 0;
   constexpr uint32_t kStep = 64 - kHeadBits<S, REV>;
   for (uint64_t q = lo; q < hi; q += kStep) {
     const uint64_t W = rd.peek(q);
@@ -375,15 +366,10 @@ __device__ __forceinline__ uint64_t plausible_start(RingReader& rd, uint64_t lo,
         else
           c += scan_block<S, DIMS, REV>(rd, c, sp);
       }
-      spent += c - (q + i);
       rd.start(ok ? q + i : q);  // the check read ahead of the window: back to it
       if (ok)
         return q + i;
-      if (spent > ZFP_SCAN_CHECK_BITS)
-        break;
     }
-    if (spent > ZFP_SCAN_CHECK_BITS)
-      break;  // give up: the segment's first bit
   }
   rd.start(lo);
   found = false;

@@ -941,12 +941,20 @@ static int run_decode4(Ctx* c, const Plan& p, S* d_field, const uint64_t* d_in, 
   HIP_TRY(hipMemcpyAsync(&n, a.ovf_count, 4, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (n) {
+    // the listed waves again, their segments staged whole: sized for sixteen
+    // worst-case blocks, so every segment fits (a wave that still did not --
+    // an index entry past the block bound -- flags an error instead of
+    // listing itself); fewer waves per CU, but only the segment's words are
+    // read, where padded slots read sixteen worst-case blocks' worth
+    const uint32_t worst = (uint32_t)((126ull + (uint64_t)kBlocks4PerWave * per_block) / 64 + 1);
+    const bool packed2 = packw && (size_t)kDec4HeadWords * 8 + (size_t)worst * 8 <= 160 * 1024 &&
+                         !getenv("ZFP_HIP_OVF_PADDED");
     if (getenv("ZFP_HIP_VERBOSE"))
-      fprintf(stderr, "zfp_hip: decode4: %u of %llu wave segments past %u staged words, decoded with padded slots\n",
-              n, (unsigned long long)nwaves, packw);
+      fprintf(stderr, "zfp_hip: decode4: %u of %llu wave segments past %u staged words, decoded %s\n", n,
+              (unsigned long long)nwaves, packw, packed2 ? "from whole segments" : "with padded slots");
     a.wave_list = a.wave_ovf;
-    a.wave_ovf = nullptr;
-    if (!launch(0, dim3(n)))
+    a.ovf_cap = 0;
+    if (!launch(packed2 ? worst : 0u, dim3(n)))
       return 0;
     a.wave_list = nullptr;
   }

@@ -201,17 +201,22 @@ def _field4(n, dtype):
     return np.stack([(f3 + 0.25 * np.cos(0.04 * w)).astype(dtype) for w in range(n)])
 
 
+@pytest.mark.parametrize("plausible", ["1", "0"])
 @pytest.mark.parametrize("n,dtype,mode,param,params", [
     (64, np.float32, "reversible", None, params_reversible()),
     (48, np.float64, "precision", 32, params_precision(32)),
 ])
-def test_scan_4d_at_scale_matches_index_and_oracle(product, oracle, n, dtype, mode, param, params):
+def test_scan_4d_at_scale_matches_index_and_oracle(product, oracle, n, dtype, mode, param, params, plausible,
+                                                   monkeypatch):
     """Regression guard for the round-3 4D scan bug (a long group section's
     reference-loop fallback restarted behind the forward-only ring reader, so
     large 4D streams were indexed wrongly): a 4D stream of tens of megabytes is
     decoded once with the encoder's index and once with none (the scan); both
     equal the oracle's decode, and the second call really scanned
-    (src/template/decompress.c:105-140 is the serial walk this replaces)."""
+    (src/template/decompress.c:105-140 is the serial walk this replaces).  With
+    pass 1's plausible chain starts and phase-A refusals (the default) and
+    without them (ZFP_HIP_SCAN_PLAUSIBLE=0)."""
+    monkeypatch.setenv("ZFP_HIP_SCAN_PLAUSIBLE", plausible)
     arr = _field4(n, dtype)
     data = product.compress(arr, mode, param)
     idx = product.last_index

@@ -82,3 +82,32 @@ def test_reference_array3_runs_unchanged_on_this_library(tmp_path, dtype, shape,
     for part in ("set.z", "set.raw", "elem.z", "elem.raw"):
         assert open(str(tmp_path / "dropin") + "." + part, "rb").read() == \
             open(str(tmp_path / "ref") + "." + part, "rb").read(), part
+
+
+CFP_REF = os.path.join(REPO, "oracle", "_ref", "cfp_check_ref")
+CFP_DROPIN = os.path.join(REPO, "oracle", "_ref", "cfp_check_dropin")
+
+
+@pytest.mark.parametrize("shape,rate", [((33, 34, 35), 8), ((20, 9, 41), 16)])
+def test_reference_cfp_runs_unchanged_on_this_library(tmp_path, shape, rate):
+    """The reference's cfp (the C bindings of its compressed arrays,
+    cfp/cfp.cpp compiled unchanged) driven from C over this libzfp.so writes the
+    same compressed bytes and values as over the reference library: array3f
+    construction, get_array, element get/set through the cache, flush
+    (cfp/cfparray3f.cpp, include/zfp/internal/cfp/array3f.h)."""
+    if not (os.path.exists(CFP_DROPIN) and os.path.exists(CFP_REF)):
+        pytest.skip("cfp checkers not built (make -C oracle ref)")
+    a = _field(shape, np.float32)
+    src = str(tmp_path / "in.raw")
+    a.tofile(src)
+    outs = {}
+    for name, exe in (("dropin", CFP_DROPIN), ("ref", CFP_REF)):
+        nz, ny, nx = shape
+        r = subprocess.run([exe, str(nx), str(ny), str(nz), str(rate), src, str(tmp_path / name)],
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout + r.stderr
+        outs[name] = r.stdout.strip()
+    assert outs["dropin"] == outs["ref"]
+    for part in ("set.z", "set.raw", "elem.z", "elem.raw"):
+        assert open(str(tmp_path / "dropin") + "." + part, "rb").read() == \
+            open(str(tmp_path / "ref") + "." + part, "rb").read(), part

@@ -15,13 +15,14 @@ R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [R, R + "/tests", R + "/oracle"]
 
 
-def field(torch, n, dtype, dev):
+def field(torch, n, dtype, dev, nz=0):
+    nz = nz or n
     x = torch.arange(n, device=dev, dtype=torch.float64)
-    out = torch.empty((n, n, n), device=dev, dtype=dtype)
+    out = torch.empty((nz, n, n), device=dev, dtype=dtype)
     base = torch.sin(0.05 * x)[None, :] * torch.cos(0.03 * x)[:, None]
     xy = 0.01 * x[None, :] * x[:, None] / n
-    for z0 in range(0, n, 64):
-        z = torch.arange(z0, min(n, z0 + 64), device=dev, dtype=torch.float64)[:, None, None]
+    for z0 in range(0, nz, 64):
+        z = torch.arange(z0, min(nz, z0 + 64), device=dev, dtype=torch.float64)[:, None, None]
         out[z0:z0 + 64] = (base[None] + 0.5 * torch.sin(0.02 * z + xy[None])).to(dtype)
     return out
 
@@ -50,6 +51,8 @@ def main():
     ap.add_argument("--dims", type=int, default=3)
     ap.add_argument("--sha", action="store_true", help="print a hash of the last stream (variant exactness)")
     ap.add_argument("--host", action="store_true", help="field and stream in host memory (PCIe-inclusive)")
+    ap.add_argument("--nz", type=int, default=0, help="3D field n x n x nz (default cubic)")
+    ap.add_argument("--header", action="store_true", help="write the 96-bit zfpy header first (C4 stream offset)")
     ap.add_argument("--lib", default=R + "/zfp-par_amd/lib/libzfp.so", help="libzfp.so to load (variant builds)")
     a = ap.parse_args()
     import torch
@@ -64,8 +67,8 @@ def main():
         f = field4(torch, a.n, dt, dev)
         zf = lib.zfp_field_4d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.n, a.n)
     else:
-        f = field(torch, a.n, dt, dev)
-        zf = lib.zfp_field_3d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.n)
+        f = field(torch, a.n, dt, dev, a.nz)
+        zf = lib.zfp_field_3d(ctypes.c_void_p(f.data_ptr()), zt, a.n, a.n, a.nz or a.n)
     if a.host:  # pinned? no: plain pageable numpy arrays, as a zfpy caller hands them over
         f = f.cpu().numpy()
         shape = [a.n] * a.dims
@@ -85,6 +88,8 @@ def main():
     ks = []
     for i in range(a.iters):
         lib.zfp_stream_rewind(zs)
+        if a.header:
+            assert lib.zfp_write_header(zs, zf, 7) == 96
         nb = lib.zfp_compress(zs, zf)
         assert nb, lib.zfp_hip_last_error()
         k, t = ctypes.c_double(), ctypes.c_double()

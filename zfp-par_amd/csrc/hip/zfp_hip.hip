@@ -1185,9 +1185,14 @@ static int copy_box(Ctx* c, const Plan& p, void* h_base, void* d_base, size_t es
 // 5 at 128 Kbit segments and 512 Kbit lead-in, 45 -> 41 ms) but not of 4D
 // reversible ones, whose unsynchronised stretches run for megabits (128^4: 91
 // passes at 64 Kbit without, 42 at 128 Kbit with, 145 -> 236 ms), so it is off
-// by default (profiles/r3_scan_lead.txt).
+// by default (profiles/r3_scan_lead.txt).  Since pass 1 starts chains at
+// plausible block starts (round 5) almost every segment is settled in pass 1,
+// whose time is the slowest lane's start search plus its parse: 32 Kbit
+// segments measured faster than 64 (128^4 reversible 38.2-39.6 -> 36.4-37.5 ms,
+// 512^3 f64 precision 32 9.7-9.8 -> 7.8-8.0 ms) and 16 Kbit slower again
+// (profiles/r5sg_scan_seg.txt, r5sg2_scan_seg_ab.txt).
 #ifndef ZFP_SCAN_MIN_SEG_BITS
-#define ZFP_SCAN_MIN_SEG_BITS 65536
+#define ZFP_SCAN_MIN_SEG_BITS 32768
 #endif
 #ifndef ZFP_SCAN_LEAD_BITS
 #define ZFP_SCAN_LEAD_BITS 0

@@ -303,12 +303,12 @@ __device__ __forceinline__ void coeffs_from_planes(int32_t (&q)[64], const uint6
     lo[k] = (uint32_t)P[k];
     hi[k] = (uint32_t)(P[k] >> 32);
   }
-  transpose32(lo);
-  transpose32(hi);
+  transpose32_dnb(lo);
+  transpose32_dnb(hi);
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    q[P3 ? kPerm3[i] : i] = (int32_t)((lo[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
-    q[P3 ? kPerm3[i + 32] : i + 32] = (int32_t)((hi[i] ^ 0xaaaaaaaau) - 0xaaaaaaaau);
+    q[P3 ? kPerm3[i] : i] = (int32_t)(lo[i] - 0xaaaaaaaau);
+    q[P3 ? kPerm3[i + 32] : i + 32] = (int32_t)(hi[i] - 0xaaaaaaaau);
   }
 }
 
@@ -321,29 +321,29 @@ __device__ __forceinline__ void coeffs_from_planes(int64_t (&q)[64], const uint6
     a[k] = (uint32_t)P[32 + k];
     b[k] = (uint32_t)(P[32 + k] >> 32);
   }
-  transpose32(a);
-  transpose32(b);
+  transpose32_dnb(a);
+  transpose32_dnb(b);
   if (__any(need_low)) {
 #pragma unroll
     for (int k = 0; k < 32; k++) {
       c[k] = (uint32_t)P[k];
       d[k] = (uint32_t)(P[k] >> 32);
     }
-    transpose32(c);
-    transpose32(d);
+    transpose32_dnb(c);
+    transpose32_dnb(d);
   } else {
 #pragma unroll
     for (int k = 0; k < 32; k++) {
-      c[k] = 0;
-      d[k] = 0;
+      c[k] = 0xaaaaaaaau;  // zero planes, odd bits inverted
+      d[k] = 0xaaaaaaaau;
     }
   }
 #pragma unroll
   for (int i = 0; i < 32; i++) {
     uint64_t u0 = ((uint64_t)a[i] << 32) | c[i];
     uint64_t u1 = ((uint64_t)b[i] << 32) | d[i];
-    q[P3 ? kPerm3[i] : i] = (int64_t)((u0 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
-    q[P3 ? kPerm3[i + 32] : i + 32] = (int64_t)((u1 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+    q[P3 ? kPerm3[i] : i] = (int64_t)(u0 - 0xaaaaaaaaaaaaaaaaull);
+    q[P3 ? kPerm3[i + 32] : i + 32] = (int64_t)(u1 - 0xaaaaaaaaaaaaaaaaull);
   }
 }
 
@@ -372,14 +372,13 @@ __device__ __forceinline__ void coeffs_from_planes_hi(int64_t (&q)[64], const ui
     a[k] = (uint32_t)P[k];
     b[k] = (uint32_t)(P[k] >> 32);
   }
-  transpose32(a);
-  transpose32(b);
+  transpose32_dnb(a);
+  transpose32_dnb(b);
 #pragma unroll
   for (int i = 0; i < 32; i++) {
-    uint64_t u0 = (uint64_t)a[i] << 32;
-    uint64_t u1 = (uint64_t)b[i] << 32;
-    q[P3 ? kPerm3[i] : i] = (int64_t)((u0 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
-    q[P3 ? kPerm3[i + 32] : i + 32] = (int64_t)((u1 ^ 0xaaaaaaaaaaaaaaaaull) - 0xaaaaaaaaaaaaaaaaull);
+    // low planes zero: (u ^ K) - K has a zero low half and high half a' - K32 (a' = a ^ K32)
+    q[P3 ? kPerm3[i] : i] = (int64_t)((uint64_t)(a[i] - 0xaaaaaaaau) << 32);
+    q[P3 ? kPerm3[i + 32] : i + 32] = (int64_t)((uint64_t)(b[i] - 0xaaaaaaaau) << 32);
   }
 }
 

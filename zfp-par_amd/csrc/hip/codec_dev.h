@@ -563,7 +563,11 @@ __device__ __forceinline__ U nb_planes(U x)
 // ---------------------------------------------------------------------------
 // Byte-granular steps are one v_perm_b32 per output word, the rest one shift
 // plus one v_bfi_b32.
-template <int J, bool INV_ODD = false>
+// INV_ODD: the encoders' last step also inverts the odd output words (odd
+// planes); ODD_BITS: the decoders' last step inverts the odd bits of every
+// output word (u ^ 0xaa..a of every coefficient, the first half of the
+// negabinary decode), in the same single bit operation.
+template <int J, bool INV_ODD = false, bool ODD_BITS = false>
 __device__ __forceinline__ void transpose_step(uint32_t (&a)[32])
 {
   constexpr uint32_t M = (J == 4) ? 0x0f0f0f0fu : (J == 2) ? 0x33333333u : 0x55555555u;
@@ -578,6 +582,9 @@ __device__ __forceinline__ void transpose_step(uint32_t (&a)[32])
     } else if constexpr (J == 8) {
       a[k] = __builtin_amdgcn_perm(y, x, 0x06020400u);
       a[k | J] = __builtin_amdgcn_perm(y, x, 0x07030501u);
+    } else if constexpr (ODD_BITS) {  // M ? first : ~second, one v_bitop3 each
+      a[k] = __builtin_amdgcn_bitop3_b32(x, y << J, M, 0xb1);
+      a[k | J] = __builtin_amdgcn_bitop3_b32(x >> J, y, M, 0xb1);
     } else {
       a[k] = (x & M) | ((y << J) & ~M);
       if constexpr (INV_ODD)  // ~(x >> J ? M : y) as one v_bitop3 (the compiler would split it)
@@ -595,6 +602,16 @@ __device__ __forceinline__ void transpose32(uint32_t (&a)[32])
   transpose_step<4>(a);
   transpose_step<2>(a);
   transpose_step<1>(a);
+}
+
+// decoder: bit planes -> coefficients u ^ K (negabinary decode: less K)
+__device__ __forceinline__ void transpose32_dnb(uint32_t (&a)[32])
+{
+  transpose_step<16>(a);
+  transpose_step<8>(a);
+  transpose_step<4>(a);
+  transpose_step<2>(a);
+  transpose_step<1, false, true>(a);
 }
 
 // encoder: coefficients x + K -> negabinary bit planes (odd planes inverted)
